@@ -1,0 +1,436 @@
+"""CPU oracle: a numpy restatement of the reference VELOCITY-ASR inference path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product package (``velocity-asr_amd/``)
+imports, links or executes this file; only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg use it, as the checker / CPU baseline.
+
+Parity pin: this restatement is checked against the golden fixtures in
+``tests/golden/`` that ``tests/golden/gen_goldens.py`` produced by running the
+real reference (``/root/reference``, torch CPU) on the same seeded inputs and
+weights (``tests/test_oracle.py``).  Every function cites the reference
+``file:line`` it restates (paths relative to the reference root).
+
+Numerics: float32 throughout, elementwise ops in the reference's order, the
+selective scan in the reference's exact (non-standard) Blelloch tree order.  Two
+forms of that tree scan are provided: the literal materialised sweep
+(``associative_scan_tree``, a line-by-line restatement of ``ssm.py:216-295``) and
+an O(log L)-state streaming form (``associative_scan_stream``) that performs the
+identical float operations in the identical order, so the two are bitwise equal
+(``tests/test_oracle.py::test_stream_equals_tree``).  The streaming form is what
+the HIP kernel implements.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+from scipy.special import erf as _erf
+
+f32 = np.float32
+
+SAMPLE_RATE = 16000
+N_FFT = 400
+HOP_LENGTH = 160
+N_MELS = 80
+
+
+# --------------------------------------------------------------------------- audio
+def hann_window(n: int = N_FFT) -> np.ndarray:
+    """torch.hann_window(n) periodic (audio.py:19, :97)."""
+    k = np.arange(n, dtype=np.float64)
+    return (0.5 - 0.5 * np.cos(2.0 * math.pi * k / n)).astype(f32)
+
+
+def _torch_linspace_f32(start: float, end: float, steps: int) -> np.ndarray:
+    """torch.linspace in float32 (ATen RangeFactories): start + i*step for the first half,
+    end - (steps-1-i)*step for the second half, each a fused multiply-add (one rounding);
+    this is what audio.py:166 and :176 evaluate."""
+    start = f32(start)
+    end = f32(end)
+    step = f32((end - start) / f32(steps - 1))
+    i = np.arange(steps)
+    half = steps // 2
+    lo = (np.float64(start) + np.float64(step) * i).astype(f32)
+    hi = (np.float64(end) - np.float64(step) * (steps - 1 - i)).astype(f32)
+    return np.where(i < half, lo, hi).astype(f32)
+
+
+def mel_filterbank(n_fft: int = N_FFT, n_mels: int = N_MELS, sample_rate: int = SAMPLE_RATE) -> np.ndarray:
+    """_create_mel_filterbank (audio.py:146-199): HTK mel, float32 ops."""
+    n_freqs = n_fft // 2 + 1
+    freqs = _torch_linspace_f32(0.0, sample_rate / 2, n_freqs)
+
+    def hz_to_mel(hz):  # audio.py:169-170
+        return f32(2595) * np.log10(f32(1) + hz / f32(700)).astype(f32)
+
+    def mel_to_hz(mel):  # audio.py:172-173
+        # torch evaluates the float32 power as a correctly rounded pow
+        return f32(700) * (np.power(10.0, (mel / f32(2595)).astype(np.float64)).astype(f32) - f32(1))
+
+    mel_min = hz_to_mel(np.array(0.0, f32))
+    mel_max = hz_to_mel(np.array(sample_rate / 2.0, f32))
+    mel_points = _torch_linspace_f32(float(mel_min), float(mel_max), n_mels + 2)
+    hz_points = mel_to_hz(mel_points).astype(f32)
+    fb = np.zeros((n_mels, n_freqs), f32)
+    for i in range(n_mels):  # audio.py:184-197
+        lower, center, upper = hz_points[i], hz_points[i + 1], hz_points[i + 2]
+        lower_slope = (freqs - lower) / (center - lower + f32(1e-10))
+        upper_slope = (upper - freqs) / (upper - center + f32(1e-10))
+        fb[i] = np.maximum(f32(0), np.minimum(lower_slope, upper_slope))
+    return fb
+
+
+def power_spectrogram(audio: np.ndarray) -> np.ndarray:
+    """Reflect pad n_fft//2, framed STFT (center=False), |X|^2 (audio.py:96-115).
+    audio (B, S) -> (B, n_fft//2+1, F)."""
+    pad = N_FFT // 2
+    xp = np.pad(audio, ((0, 0), (pad, pad)), mode="reflect")
+    F = (xp.shape[1] - N_FFT) // HOP_LENGTH + 1
+    idx = np.arange(F)[:, None] * HOP_LENGTH + np.arange(N_FFT)[None, :]
+    frames = xp[:, idx] * hann_window()[None, None, :]
+    X = np.fft.rfft(frames.astype(f32), axis=-1)
+    mag = np.abs(X).astype(f32)
+    return np.transpose(mag * mag, (0, 2, 1)).astype(f32)
+
+
+def compute_mel_spectrogram(audio: np.ndarray, normalize: bool = True) -> np.ndarray:
+    """compute_mel_spectrogram (audio.py:65-143): (S,)|(B,S) -> (F,80)|(B,F,80)."""
+    audio = np.asarray(audio, f32)
+    squeeze = audio.ndim == 1
+    if squeeze:
+        audio = audio[None]
+    P = power_spectrogram(audio)
+    mel = np.matmul(mel_filterbank()[None], P).astype(f32)           # audio.py:126
+    mel = np.log(mel + f32(1e-10)).astype(f32)                       # audio.py:129
+    if normalize:                                                    # audio.py:132-135
+        mean = mel.astype(np.float64).mean(axis=-1, keepdims=True).astype(f32)
+        std = mel.astype(np.float64).std(axis=-1, ddof=1, keepdims=True).astype(f32)
+        mel = ((mel - mean) / (std + f32(1e-10))).astype(f32)
+    mel = np.transpose(mel, (0, 2, 1))
+    return np.ascontiguousarray(mel[0] if squeeze else mel)
+
+
+# --------------------------------------------------------------------------- layers
+def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float = 1e-5) -> np.ndarray:
+    """nn.LayerNorm (biased variance, eps 1e-5)."""
+    mean = x.mean(axis=-1, keepdims=True, dtype=np.float64)
+    var = ((x.astype(np.float64) - mean) ** 2).mean(axis=-1, keepdims=True)
+    y = ((x - mean.astype(f32)) * (1.0 / np.sqrt(var + eps)).astype(f32)).astype(f32)
+    return (y * w + b).astype(f32)
+
+
+def gelu(x: np.ndarray) -> np.ndarray:
+    """nn.GELU() exact erf form."""
+    x = x.astype(f32)
+    return (f32(0.5) * x * (f32(1) + _erf(x / f32(math.sqrt(2.0))).astype(f32))).astype(f32)
+
+
+def softplus(x: np.ndarray) -> np.ndarray:
+    """F.softplus(beta=1, threshold=20) (ssm.py:113)."""
+    x = x.astype(f32)
+    return np.where(x > 20, x, np.log1p(np.exp(np.minimum(x, 20)))).astype(f32)
+
+
+def silu(x: np.ndarray) -> np.ndarray:
+    x = x.astype(f32)
+    return (x / (f32(1) + np.exp(-x))).astype(f32)
+
+
+def sigmoid(x: np.ndarray) -> np.ndarray:
+    x = x.astype(f32)
+    return (f32(1) / (f32(1) + np.exp(-x))).astype(f32)
+
+
+def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None) -> np.ndarray:
+    y = np.matmul(x, w.T).astype(f32)
+    if b is not None:
+        y = (y + b).astype(f32)
+    return y
+
+
+def conv1d_k3s2(x: np.ndarray, w: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """TemporalBindingLayer.conv (model.py:156-162): Conv1d(80->D, k3, s2, p1) on
+    (B, F, C) input, returned as (B, L, D)."""
+    B, F, C = x.shape
+    L = (F + 2 - 3) // 2 + 1
+    xp = np.zeros((B, F + 2, C), f32)
+    xp[:, 1:F + 1] = x
+    cols = np.concatenate([xp[:, k:k + 2 * L:2][:, :L] for k in range(3)], axis=-1)  # (B,L,3C) [k-major]
+    wm = np.transpose(w, (0, 2, 1)).reshape(w.shape[0], -1)                           # (D, 3C) [k-major]
+    return (np.matmul(cols, wm.T) + b).astype(f32)
+
+
+def causal_dwconv(x: np.ndarray, w: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Depthwise Conv1d(k, padding=k-1) keeping the first L outputs (ssm.py:377-383,
+    :411-414): y[t,c] = b[c] + sum_j w[c,0,j] * x[t-(k-1)+j, c]."""
+    B, L, C = x.shape
+    k = w.shape[-1]
+    xp = np.concatenate([np.zeros((B, k - 1, C), f32), x], axis=1)
+    y = np.zeros((B, L, C), f32)
+    for j in range(k):
+        y = (y + xp[:, j:j + L] * w[:, 0, j]).astype(f32)
+    return (y + b).astype(f32)
+
+
+# --------------------------------------------------------------------------- scans
+def sequential_scan(x, dt, A, Bm, Cm, D):
+    """_sequential_scan (ssm.py:134-171): true recurrence h_t = dA_t h_{t-1} + x_t dB_t,
+    y_t = <h_t, C_t> + x_t D."""
+    Bsz, L, Di = x.shape
+    N = A.shape[0]
+    h = np.zeros((Bsz, Di, N), f32)
+    y = np.empty_like(x)
+    for t in range(L):
+        dA = np.exp(dt[:, t, :, None] * A[None, None, :]).astype(f32)
+        dB = (dt[:, t, :, None] * Bm[:, t, None, :]).astype(f32)
+        h = (dA * h + x[:, t, :, None] * dB).astype(f32)
+        y[:, t] = np.einsum("bdn,bn->bd", h, Cm[:, t]).astype(f32)
+    return (y + x * D).astype(f32)
+
+
+def discretize(x, dt, A, Bm):
+    """_parallel_scan discretisation (ssm.py:196-202): dA = exp(dt*A), x_dB = x*(dt*B)."""
+    dA = np.exp(dt[..., None] * A).astype(f32)
+    dB = (dt[..., None] * Bm[:, :, None, :]).astype(f32)
+    return dA, (x[..., None] * dB).astype(f32)
+
+
+def associative_scan_tree(dA: np.ndarray, xdB: np.ndarray) -> np.ndarray:
+    """Literal restatement of _associative_scan (ssm.py:216-295) over axis 1.
+
+    Up-sweep (a_r, b_r) <- (a_r*a_l, a_r*b_l + b_r); root <- (1, 0); down-sweep
+    left <- right, a_r <- a_r*a_l_old, b_r <- a_r(new)*b_l_old + b_r.  Returns b[:, :L]:
+    the reference's exclusive, mis-combined prefix."""
+    L = dA.shape[1]
+    log_len = int(math.ceil(math.log2(max(L, 1))))
+    P = 2 ** log_len
+    a = np.ones((dA.shape[0], P) + dA.shape[2:], f32)
+    b = np.zeros_like(a)
+    a[:, :L] = dA
+    b[:, :L] = xdB
+    stride = 1
+    for _ in range(log_len):                       # ssm.py:244-261
+        s2 = stride * 2
+        r = np.arange(s2 - 1, P, s2)
+        l = r - stride
+        al, bl, ar, br = a[:, l], b[:, l], a[:, r], b[:, r]
+        a[:, r] = ar * al
+        b[:, r] = ar * bl + br
+        stride = s2
+    a[:, -1] = 1.0                                 # ssm.py:264-265
+    b[:, -1] = 0.0
+    stride = P // 2
+    for _ in range(log_len):                       # ssm.py:267-286
+        s2 = stride * 2
+        r = np.arange(s2 - 1, P, s2)
+        l = r - stride
+        al_old = a[:, l].copy()
+        bl_old = b[:, l].copy()
+        a[:, l] = a[:, r]
+        b[:, l] = b[:, r]
+        a[:, r] = a[:, r] * al_old
+        b[:, r] = a[:, r] * bl_old + b[:, r]
+        stride //= 2
+    return b[:, :L]
+
+
+def associative_scan_stream(dA: np.ndarray, xdB: np.ndarray) -> np.ndarray:
+    """Streaming form of associative_scan_tree with a binary-counter stack of aligned
+    blocks (la, lb: up-sweep composite; ca, cb: down-sweep prefix after the block).
+    Same float operations in the same order, so bitwise equal to the tree."""
+    L = dA.shape[1]
+    out = np.empty_like(xdB)
+    stack: List[list] = []  # entries [lvl, la, lb, ca, cb]
+    zero = np.zeros_like(xdB[:, 0])
+    for t in range(L):
+        out[:, t] = stack[-1][4] if stack else zero
+        la, lb, lvl = dA[:, t], xdB[:, t], 0
+        while stack and stack[-1][0] == lvl:          # up-sweep merge with left sibling
+            _, pla, plb, _, _ = stack.pop()
+            lb = la * plb + lb
+            la = la * pla
+            lvl += 1
+        if stack:                                     # down-sweep prefix through this block
+            pa, pb = stack[-1][3], stack[-1][4]
+            ca = pa * la
+            cb = ca * lb + pb
+        else:
+            ca = la * np.float32(1.0)
+            cb = ca * lb
+        stack.append([lvl, la, lb, ca, cb])
+    return out
+
+
+def parallel_scan(x, dt, A, Bm, Cm, D, stream: bool = True):
+    """_parallel_scan (ssm.py:173-214): y = einsum(h, C) + x*D with the tree scan."""
+    dA, xdB = discretize(x, dt, A, Bm)
+    h = associative_scan_stream(dA, xdB) if stream else associative_scan_tree(dA, xdB)
+    y = np.einsum("bldn,bln->bld", h, Cm).astype(f32)
+    return (y + x * D).astype(f32)
+
+
+# --------------------------------------------------------------------------- blocks
+def selective_ssm(W: Dict[str, np.ndarray], p: str, x: np.ndarray, mode: str) -> np.ndarray:
+    """SelectiveSSM.forward (ssm.py:92-132)."""
+    Di = W[p + "D"].shape[0]
+    xz = linear(x, W[p + "in_proj.weight"])
+    xp, z = xz[..., :Di], xz[..., Di:]
+    xdbl = linear(xp, W[p + "x_proj.weight"])
+    N = xdbl.shape[-1] // 2
+    Bm, Cm = xdbl[..., :N], xdbl[..., N:]
+    dt = softplus(linear(xp, W[p + "dt_proj.weight"], W[p + "dt_proj.bias"]))
+    A = (-np.exp(W[p + "A_log"])).astype(f32)
+    if mode == "sequential":
+        y = sequential_scan(xp, dt, A, Bm, Cm, W[p + "D"])
+    elif mode == "parallel":
+        y = parallel_scan(xp, dt, A, Bm, Cm, W[p + "D"])
+    else:
+        raise ValueError(f"Unknown scan_mode: {mode}")
+    y = (y * silu(z)).astype(f32)
+    return linear(y, W[p + "out_proj.weight"])
+
+
+def ssm_block(W, p: str, x: np.ndarray, mode: str) -> np.ndarray:
+    """SSMBlock._forward_impl (ssm.py:404-427); dropout is identity in eval."""
+    r = x
+    h = layer_norm(x, W[p + "norm1.weight"], W[p + "norm1.bias"])
+    h = causal_dwconv(h, W[p + "conv.weight"], W[p + "conv.bias"])
+    x = (selective_ssm(W, p + "ssm.", h, mode) + r).astype(f32)
+    r = x
+    h = layer_norm(x, W[p + "norm2.weight"], W[p + "norm2.bias"])
+    h = gelu(linear(h, W[p + "ffn.0.weight"], W[p + "ffn.0.bias"]))
+    h = linear(h, W[p + "ffn.3.weight"], W[p + "ffn.3.bias"])
+    return (h + r).astype(f32)
+
+
+def temporal_binding(W, mel: np.ndarray) -> np.ndarray:
+    """TemporalBindingLayer.forward (model.py:176-202) + PositionalEncoding2D (:106-127)."""
+    x = gelu(conv1d_k3s2(mel, W["temporal_binding.conv.weight"], W["temporal_binding.conv.bias"]))
+    L = x.shape[1]
+    pe_t = W["temporal_binding.pos_encoding.pe_time"][:L]
+    pe_f = np.broadcast_to(W["temporal_binding.pos_encoding.pe_freq"][0], (L, pe_t.shape[1]))
+    x = (x + np.concatenate([pe_t, pe_f], axis=-1)[None]).astype(f32)
+    return layer_norm(x, W["temporal_binding.norm.weight"], W["temporal_binding.norm.bias"])
+
+
+def pool_sizes(L: int) -> Tuple[int, int]:
+    """AdaptivePool._compute_pool_size + clamp to seq_len (attention.py:37-44, :67)."""
+    k1 = min(max(64, L // 8), L)
+    k2 = min(min(64, max(16, k1 // 4)), k1)
+    return k1, k2
+
+
+def adaptive_avg_pool(x: np.ndarray, K: int) -> np.ndarray:
+    """F.adaptive_avg_pool1d over time: bin i = [floor(iL/K), ceil((i+1)L/K))."""
+    B, L, C = x.shape
+    out = np.empty((B, K, C), f32)
+    for i in range(K):
+        s = (i * L) // K
+        e = -((-(i + 1) * L) // K)
+        out[:, i] = (x[:, s:e].sum(axis=1, dtype=f32) / f32(e - s)).astype(f32)
+    return out
+
+
+def multi_head_attention(W, p: str, q_in, kv_in, heads: int) -> np.ndarray:
+    """MultiHeadAttention.forward (attention.py:116-164), mask=None."""
+    q = linear(q_in, W[p + "q_proj.weight"], W[p + "q_proj.bias"])
+    k = linear(kv_in, W[p + "k_proj.weight"], W[p + "k_proj.bias"])
+    v = linear(kv_in, W[p + "v_proj.weight"], W[p + "v_proj.bias"])
+    B, Lq, A = q.shape
+    hd = A // heads
+    qh = q.reshape(B, Lq, heads, hd).transpose(0, 2, 1, 3)
+    kh = k.reshape(B, -1, heads, hd).transpose(0, 2, 1, 3)
+    vh = v.reshape(B, -1, heads, hd).transpose(0, 2, 1, 3)
+    s = (np.matmul(qh, kh.transpose(0, 1, 3, 2)) / f32(math.sqrt(hd))).astype(f32)
+    s = s - s.max(axis=-1, keepdims=True)
+    e = np.exp(s).astype(f32)
+    attn = (e / e.sum(axis=-1, keepdims=True)).astype(f32)
+    o = np.matmul(attn, vh).astype(f32).transpose(0, 2, 1, 3).reshape(B, Lq, A)
+    return linear(o, W[p + "out_proj.weight"], W[p + "out_proj.bias"])
+
+
+def gated_fusion(W, p: str, local, glob) -> np.ndarray:
+    """GatedFusion.forward (attention.py:191-220)."""
+    g = sigmoid(linear(np.concatenate([local, glob], axis=-1), W[p + "gate_proj.0.weight"],
+                       W[p + "gate_proj.0.bias"]))
+    lt = linear(local, W[p + "local_proj.weight"], W[p + "local_proj.bias"])
+    gt = linear(glob, W[p + "global_proj.weight"], W[p + "global_proj.bias"])
+    fused = (g * lt + (f32(1) - g) * gt).astype(f32)
+    return linear(fused, W[p + "out_proj.weight"], W[p + "out_proj.bias"])
+
+
+def global_context(W, local: np.ndarray, cfg: dict) -> np.ndarray:
+    """HierarchicalGlobalContext.forward (attention.py:283-319)."""
+    g = "global_context."
+    L = local.shape[1]
+    k1, _ = pool_sizes(L)
+    x = linear(adaptive_avg_pool(local, k1), W[g + "pool1.pool_proj.weight"], W[g + "pool1.pool_proj.bias"])
+    for i in range(cfg["global_ssm_layers"]):
+        x = ssm_block(W, f"{g}global_ssm.layers.{i}.", x, "parallel")   # GlobalSSM: always parallel
+    x = layer_norm(x, W[g + "global_ssm.norm.weight"], W[g + "global_ssm.norm.bias"])
+    k2 = min(min(64, max(16, k1 // 4)), x.shape[1])
+    x2 = linear(adaptive_avg_pool(x, k2), W[g + "pool2.pool_proj.weight"], W[g + "pool2.pool_proj.bias"])
+    x2 = layer_norm(x2, W[g + "norm1.weight"], W[g + "norm1.bias"])
+    q = layer_norm(local, W[g + "norm2.weight"], W[g + "norm2.bias"])
+    ctx = multi_head_attention(W, g + "cross_attention.", q, x2, cfg["attention_heads"])
+    return gated_fusion(W, g + "fusion.", local, ctx)
+
+
+def forward(W: Dict[str, np.ndarray], mel: np.ndarray, cfg: dict, return_features: bool = False):
+    """VELOCITYASR.forward (model.py:333-368): (B, F, mel_bins) -> (B, L, V)."""
+    x = temporal_binding(W, np.asarray(mel, f32))
+    tb = x
+    for i in range(cfg["ssm_layers"]):
+        x = ssm_block(W, f"local_ssm.layers.{i}.", x, cfg["scan_mode"])
+    local = layer_norm(x, W["local_ssm.norm.weight"], W["local_ssm.norm.bias"])
+    fused = global_context(W, local, cfg)
+    h = layer_norm(fused, W["ctc_head.proj.0.weight"], W["ctc_head.proj.0.bias"])
+    logits = linear(h, W["ctc_head.proj.2.weight"], W["ctc_head.proj.2.bias"])
+    if return_features:
+        return logits, dict(temporal_binding=tb, local_features=local, fused_features=fused)
+    return logits
+
+
+# --------------------------------------------------------------------------- decode
+def ctc_greedy_decode(logits: np.ndarray, blank: int = 0, collapse_repeated: bool = True) -> List[List[int]]:
+    """ctc_greedy_decode (decode.py:27-71); argmax ties resolve to the first index."""
+    pred = np.argmax(logits, axis=-1)
+    out = []
+    for row in pred.tolist():
+        toks, prev = [], None
+        for tok in row:
+            if tok == blank:
+                prev = None
+                continue
+            if collapse_repeated and tok == prev:
+                continue
+            toks.append(tok)
+            prev = tok
+        out.append(toks)
+    return out
+
+
+def ctc_greedy_decode_with_timestamps(logits: np.ndarray, blank: int = 0):
+    """ctc_greedy_decode_with_timestamps (decode.py:74-125)."""
+    pred = np.argmax(logits, axis=-1)
+    results = []
+    for row in pred.tolist():
+        toks, ts, prev, start = [], [], None, 0
+        for i, tok in enumerate(row):
+            if tok == blank:
+                if prev is not None and prev != blank:
+                    ts.append((start, i))
+                prev = tok
+                continue
+            if tok != prev:
+                if prev is not None and prev != blank:
+                    ts.append((start, i))
+                toks.append(tok)
+                start = i
+            prev = tok
+        if prev is not None and prev != blank:
+            ts.append((start, len(row)))
+        results.append((toks, ts))
+    return results

@@ -1,0 +1,320 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REAL reference.
+
+Container-only tool (the reference tree does not exist on the GPU box).  Run as
+
+    PYTHONDONTWRITEBYTECODE=1 PYTHONPATH=/root/reference \
+        python tests/golden/gen_goldens.py
+
+It imports the reference ``velocity_asr`` package read-only, loads the portable
+weight recipe (``velocity-asr_amd/velocity_asr/synthetic.py``) by file path, runs
+the reference CPU path on seeded inputs and writes small .npz/.json fixtures
+(inputs are regenerated from the recorded seeds; only outputs and small inputs
+are stored).  Every file records the torch version, thread count and batch
+shape, because the reference CPU path is not batch-invariant at the 1e-6 level
+("Batch-invariance").
+"""
+
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+SYN_PATH = os.path.join(REPO, "velocity-asr_amd", "velocity_asr", "synthetic.py")
+
+spec = importlib.util.spec_from_file_location("vasr_synthetic", SYN_PATH)
+syn = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(syn)
+
+import velocity_asr as ref  # noqa: E402  (the reference, via PYTHONPATH)
+from velocity_asr import audio as ref_audio  # noqa: E402
+from velocity_asr import decode as ref_decode  # noqa: E402
+from velocity_asr import training as ref_training  # noqa: E402
+from velocity_asr.ssm import SelectiveSSM  # noqa: E402
+
+assert os.path.realpath(os.path.dirname(ref.__file__)).startswith("/root/reference"), ref.__file__
+
+torch.set_num_threads(8)
+META = dict(torch=torch.__version__, threads=torch.get_num_threads(), numpy=np.__version__)
+
+
+def build_model(config=None, seed=0):
+    cfg = ref.VelocityASRConfig(**(config or {}))
+    model = ref.VELOCITYASR(cfg)
+    weights = syn.make_weights(config, seed=seed)
+    sd = model.state_dict()
+    assert list(sd.keys()) == list(weights.keys()), "recipe key order != reference state_dict"
+    for k, v in sd.items():
+        assert tuple(v.shape) == weights[k].shape, (k, v.shape, weights[k].shape)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in weights.items()}, strict=True)
+    model.eval()
+    return model
+
+
+def meta(**kw):
+    d = dict(META)
+    d.update(kw)
+    return np.array(json.dumps(d))
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {name}: {os.path.getsize(path)/1024:.1f} KiB")
+
+
+# --------------------------------------------------------------------------- mel
+def gen_mel():
+    out = {}
+    cases = {
+        "rand_b2_1s": syn.make_audio(2, 16000, seed=11),
+        "rand_b2_10s": syn.make_audio(2, 160000, seed=1234),
+        "chirp_3s": syn.make_chirp(48000)[None],
+        "zero_1s": np.zeros((1, 16000), np.float32),
+        "short_201": syn.make_audio(1, 201, seed=5),
+        "short_400": syn.make_audio(1, 400, seed=6),
+        "odd_16333": syn.make_audio(3, 16333, seed=8),
+    }
+    for name, audio in cases.items():
+        with torch.no_grad():
+            mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(audio))
+        out[name] = mel.numpy()
+        if name in ("chirp_3s", "zero_1s", "short_201", "short_400"):
+            out[name + "__audio"] = audio
+    # 1-D input squeezes (audio.py:89-91, 140-141)
+    a1 = syn.make_audio(1, 8000, seed=9)[0]
+    out["oned_8000"] = ref_audio.compute_mel_spectrogram(torch.from_numpy(a1)).numpy()
+    fb = ref_audio._create_mel_filterbank(400, 80, 16000, torch.device("cpu"))
+    out["filterbank"] = fb.numpy()
+    out["hann"] = torch.hann_window(400).numpy()
+    out["meta"] = meta(seeds=dict(rand_b2_1s=11, rand_b2_10s=1234, short_201=5, short_400=6,
+                                  odd_16333=8, oned_8000=9, chirp=7))
+    save("mel.npz", **out)
+
+
+# --------------------------------------------------------------------------- scan
+def scan_inputs(seed, B, L, Di, N):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B, L, Di)).astype(np.float32)
+    dt = np.log1p(np.exp(rng.standard_normal((B, L, Di)) * 0.7 - 1.0)).astype(np.float32)
+    Bm = rng.standard_normal((B, L, N)).astype(np.float32)
+    Cm = rng.standard_normal((B, L, N)).astype(np.float32)
+    A_log = (np.log(np.arange(1, N + 1)) + 0.01 * rng.standard_normal(N)).astype(np.float32)
+    D = (1.0 + 0.1 * rng.standard_normal(Di)).astype(np.float32)
+    return x, dt, Bm, Cm, A_log, D
+
+
+SCAN_CASES = [
+    # (name, seed, B, L, Di, N)
+    ("L1", 100, 2, 1, 8, 64),
+    ("L2", 101, 2, 2, 8, 64),
+    ("L3", 102, 2, 3, 8, 64),
+    ("L7", 103, 1, 7, 16, 64),
+    ("L16", 104, 1, 16, 8, 64),
+    ("L17", 105, 1, 17, 8, 64),
+    ("L64_N32", 106, 2, 64, 16, 32),
+    ("L100", 107, 1, 100, 8, 64),
+    ("L187_N32", 108, 1, 187, 8, 32),
+    ("L501", 109, 2, 501, 8, 64),
+    ("L1501", 110, 1, 1501, 4, 64),
+]
+
+
+def gen_scan():
+    out = {}
+    for name, seed, B, L, Di, N in SCAN_CASES:
+        x, dt, Bm, Cm, A_log, D = scan_inputs(seed, B, L, Di, N)
+        ssm = SelectiveSSM(d_model=Di // 2, state_dim=N, expand_ratio=2)
+        with torch.no_grad():
+            ssm.D.copy_(torch.from_numpy(D))
+            A = -torch.exp(torch.from_numpy(A_log))
+            tx, tdt, tB, tC = (torch.from_numpy(v) for v in (x, dt, Bm, Cm))
+            yp = ssm._parallel_scan(tx, tdt, A, tB, tC)
+            ys = ssm._sequential_scan(tx, tdt, A, tB, tC)
+        out[name + "__parallel"] = yp.numpy()
+        out[name + "__sequential"] = ys.numpy()
+    out["meta"] = meta(cases=[list(c) for c in SCAN_CASES],
+                       inputs="tests/golden/gen_goldens.py:scan_inputs(seed,B,L,Di,N)")
+    save("scan.npz", **out)
+
+
+# --------------------------------------------------------------------------- forward
+def topk_pack(prefix, logits, out, every=25):
+    lg = torch.from_numpy(logits) if isinstance(logits, np.ndarray) else logits
+    vals, idx = torch.topk(lg, 5, dim=-1)
+    out[prefix + "tokens"] = lg.argmax(-1).numpy().astype(np.int32)
+    out[prefix + "top5_val"] = vals.numpy()
+    out[prefix + "top5_idx"] = idx.numpy().astype(np.int32)
+    out[prefix + "frames"] = np.arange(0, lg.shape[1], every, dtype=np.int32)
+    out[prefix + "logits_sub"] = lg[:, ::every].numpy()
+    out[prefix + "margin_min"] = np.array((vals[..., 0] - vals[..., 1]).min().item(), np.float32)
+    out[prefix + "abs_sum"] = lg.abs().sum(dim=(1, 2)).double().numpy()
+
+
+def run_forward(model, audio):
+    with torch.no_grad():
+        mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(audio))
+        logits, feats = model(mel, return_features=True)
+    return mel, logits, feats
+
+
+def greedy_json(logits):
+    return ref_decode.ctc_greedy_decode(logits)
+
+
+def gen_forward():
+    model = build_model()
+    decoded = {}
+
+    # (i) per-stage features at B=2 x 3 s
+    audio = syn.make_audio(2, 48000, seed=21)
+    mel, logits, feats = run_forward(model, audio)
+    save("fwd_b2_3s.npz", mel=mel.numpy(), temporal_binding=feats["temporal_binding"].numpy(),
+         local_features=feats["local_features"].numpy(),
+         fused_features=feats["fused_features"].numpy(), logits=logits.numpy(),
+         tokens=logits.argmax(-1).numpy().astype(np.int32),
+         meta=meta(audio="make_audio(2, 48000, seed=21)", weights="make_weights(None, seed=0)",
+                   batch=[2, 48000]))
+    decoded["b2_3s"] = greedy_json(logits)
+    decoded["b2_3s_ts"] = ref_decode.ctc_greedy_decode_with_timestamps(logits)
+
+    # (ii) headline shape, two utterances of 10 s
+    audio = syn.make_audio(2, 160000, seed=1234)
+    mel, logits, feats = run_forward(model, audio)
+    out = {}
+    topk_pack("", logits, out)
+    out["local_sub"] = feats["local_features"][:, ::25].numpy()
+    out["meta"] = meta(audio="make_audio(2, 160000, seed=1234)", weights="make_weights(None, seed=0)",
+                       batch=[2, 160000])
+    save("fwd_b2_10s.npz", **out)
+    decoded["b2_10s"] = greedy_json(logits)
+
+    # (iii) long utterance, 30 s (L=1501, P=2048, K1=187, K2=46)
+    audio = syn.make_audio(1, 480000, seed=4321)
+    mel, logits, feats = run_forward(model, audio)
+    out = {}
+    topk_pack("", logits, out, every=50)
+    out["meta"] = meta(audio="make_audio(1, 480000, seed=4321)", weights="make_weights(None, seed=0)",
+                       batch=[1, 480000])
+    save("fwd_b1_30s.npz", **out)
+    decoded["b1_30s"] = greedy_json(logits)
+
+    # (iv) chirp 'speech-like' clip, B=1 x 3 s
+    audio = syn.make_chirp(48000)[None]
+    mel, logits, feats = run_forward(model, audio)
+    save("fwd_chirp_3s.npz", logits=logits.numpy(), tokens=logits.argmax(-1).numpy().astype(np.int32),
+         meta=meta(audio="make_chirp(48000)[None]", batch=[1, 48000]))
+    decoded["chirp_3s"] = greedy_json(logits)
+
+    # (v) edge lengths: L = 1, 2, 6, 26, 51; pool sizes clamp to L
+    edge = {}
+    for S, seed in ((201, 31), (400, 32), (1600, 33), (8000, 34), (16333, 35)):
+        audio = syn.make_audio(1, S, seed=seed)
+        mel, logits, feats = run_forward(model, audio)
+        edge[f"S{S}__logits"] = logits.numpy()
+        edge[f"S{S}__tokens"] = logits.argmax(-1).numpy().astype(np.int32)
+    edge["meta"] = meta(audio="make_audio(1, S, seed) for (S, seed) in (201,31),(400,32),(1600,33),(8000,34),(16333,35)")
+    save("fwd_edge.npz", **edge)
+
+    # (vi) raw-mel input (model API takes mel, not audio): randn mel like test_vel.py
+    rng = np.random.default_rng(41)
+    mel_in = rng.standard_normal((2, 500, 80)).astype(np.float32)
+    with torch.no_grad():
+        logits = model(torch.from_numpy(mel_in))
+    save("fwd_melin_500.npz", logits=logits.numpy(), tokens=logits.argmax(-1).numpy().astype(np.int32),
+         meta=meta(mel="default_rng(41).standard_normal((2,500,80))", batch=[2, 500]))
+
+    with open(os.path.join(HERE, "decode_fwd.json"), "w") as f:
+        json.dump({"meta": json.loads(str(meta())), "results": decoded}, f)
+    print("wrote decode_fwd.json")
+
+
+def gen_forward_sequential():
+    cfg = dict(scan_mode="sequential")
+    model = build_model(cfg)
+    audio = syn.make_audio(2, 48000, seed=21)
+    mel, logits, feats = run_forward(model, audio)
+    save("fwd_seq_b2_3s.npz", logits=logits.numpy(), local_features=feats["local_features"].numpy(),
+         tokens=logits.argmax(-1).numpy().astype(np.int32),
+         meta=meta(config=cfg, audio="make_audio(2, 48000, seed=21)", batch=[2, 48000]))
+
+
+SMALL_CFG = dict(d_model=96, ssm_layers=2, ssm_state_dim=32, global_ssm_state_dim=16,
+                 attention_heads=2, attention_dim=24, vocab_size=50)
+
+
+def gen_forward_small_config():
+    model = build_model(SMALL_CFG, seed=3)
+    audio = syn.make_audio(2, 32000, seed=51)
+    mel, logits, feats = run_forward(model, audio)
+    save("fwd_smallcfg.npz", logits=logits.numpy(), tokens=logits.argmax(-1).numpy().astype(np.int32),
+         local_features=feats["local_features"].numpy(),
+         meta=meta(config=SMALL_CFG, weights_seed=3, audio="make_audio(2, 32000, seed=51)",
+                   batch=[2, 32000]))
+
+
+# --------------------------------------------------------------------------- decode / wer
+def gen_decode():
+    rng = np.random.default_rng(61)
+    cases = {}
+    # sticky random token streams with blanks and repeats, V=12
+    for i, (B, L, V) in enumerate(((3, 40, 12), (2, 1, 5), (1, 64, 3), (2, 33, 1000))):
+        toks = np.zeros((B, L), np.int64)
+        for b in range(B):
+            cur = 0
+            for t in range(L):
+                r = rng.random()
+                if r < 0.3:
+                    cur = 0
+                elif r < 0.6:
+                    cur = int(rng.integers(0, V))
+                toks[b, t] = cur
+        logits = rng.standard_normal((B, L, V)).astype(np.float32)
+        # make the chosen token the argmax
+        logits[np.arange(B)[:, None], np.arange(L)[None], toks] = 10.0
+        lt = torch.from_numpy(logits)
+        cases[f"c{i}"] = dict(
+            logits=logits.tolist(),
+            greedy=ref_decode.ctc_greedy_decode(lt),
+            greedy_nocollapse=ref_decode.ctc_greedy_decode(lt, collapse_repeated=False),
+            timestamps=[[list(tk), [list(s) for s in ts]] for tk, ts in
+                        ref_decode.ctc_greedy_decode_with_timestamps(lt)],
+        )
+    vocab = ref_decode.create_default_vocabulary(1000)
+    dec = ref_decode.CTCDecoder(vocab)
+    texts = dec.decode_greedy(torch.from_numpy(np.array(cases["c3"]["logits"], np.float32)))
+    wer_cases = [
+        (["the cat sat", "hello world"], ["the cat sat on", "hello word"]),
+        ([""], ["a b c"]),
+        (["A B"], ["a b"]),
+        (["x y z"], [""]),
+    ]
+    wer = [dict(pred=p, ref=r, wer=ref_training.compute_wer(p, r), cer=ref_training.compute_cer(p, r))
+           for p, r in wer_cases]
+    out = dict(meta=json.loads(str(meta())), cases=cases, vocab_head=vocab[:80], vocab_len=len(vocab),
+               vocab_tail=vocab[-3:], texts_c3=texts, wer=wer,
+               vocab_small=ref_decode.create_default_vocabulary(10))
+    with open(os.path.join(HERE, "decode.json"), "w") as f:
+        json.dump(out, f)
+    print("wrote decode.json")
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode"]
+    if "mel" in which:
+        gen_mel()
+    if "scan" in which:
+        gen_scan()
+    if "forward" in which:
+        gen_forward()
+    if "sequential" in which:
+        gen_forward_sequential()
+    if "small" in which:
+        gen_forward_small_config()
+    if "decode" in which:
+        gen_decode()

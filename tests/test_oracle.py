@@ -1,0 +1,173 @@
+"""Pin the CPU oracle (oracle/velocity_ref.py) to the reference's golden outputs.
+
+The goldens were produced by the real reference (tests/golden/gen_goldens.py), so
+these tests are what makes the oracle trustworthy as the checker for the HIP path.
+"""
+
+import json
+
+import numpy as np
+import pytest
+
+from conftest import golden, golden_json
+from oracle import velocity_ref as R
+from velocity_asr import synthetic as S
+
+FWD_TOL = dict(atol=1e-4, rtol=1e-4)
+
+
+def test_window_and_filterbank_match_reference():
+    g = golden("mel.npz")
+    np.testing.assert_allclose(R.hann_window(), g["hann"], atol=5e-7, rtol=0)
+    fb = R.mel_filterbank()
+    assert fb.shape == (80, 201)
+    np.testing.assert_array_equal(fb, g["filterbank"])  # bit-exact restatement
+    # 393 non-zeros, 1-14 per row
+    assert int((g["filterbank"] > 0).sum()) == 393
+
+
+@pytest.mark.parametrize("name,make", [
+    ("rand_b2_1s", lambda: S.make_audio(2, 16000, seed=11)),
+    ("rand_b2_10s", lambda: S.make_audio(2, 160000, seed=1234)),
+    ("odd_16333", lambda: S.make_audio(3, 16333, seed=8)),
+    ("chirp_3s", lambda: S.make_chirp(48000)[None]),
+    ("zero_1s", lambda: np.zeros((1, 16000), np.float32)),
+    ("short_201", lambda: S.make_audio(1, 201, seed=5)),
+    ("short_400", lambda: S.make_audio(1, 400, seed=6)),
+    ("oned_8000", lambda: S.make_audio(1, 8000, seed=9)[0]),
+])
+def test_mel_matches_reference(name, make):
+    g = golden("mel.npz")
+    audio = make()
+    if name + "__audio" in g.files:
+        np.testing.assert_array_equal(audio.reshape(g[name + "__audio"].shape), g[name + "__audio"])
+    mel = R.compute_mel_spectrogram(audio)
+    assert mel.shape == g[name].shape
+    np.testing.assert_allclose(mel, g[name], atol=2e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 5, 8, 16, 17, 31, 64, 100, 257])
+def test_stream_equals_tree_bitwise(L):
+    rng = np.random.default_rng(L)
+    dA = np.exp(-rng.random((2, L, 3, 4)) * 3).astype(np.float32)
+    xdB = rng.standard_normal((2, L, 3, 4)).astype(np.float32)
+    tree = R.associative_scan_tree(dA, xdB)
+    stream = R.associative_scan_stream(dA, xdB)
+    np.testing.assert_array_equal(stream, tree)
+    assert np.all(tree[:, 0] == 0)  # exclusive prefix: h[0] = 0
+
+
+def _scan_cases():
+    meta = json.loads(str(golden("scan.npz")["meta"]))
+    return [tuple(c) for c in meta["cases"]]
+
+
+@pytest.mark.parametrize("case", _scan_cases(), ids=lambda c: c[0])
+def test_scan_matches_reference(case):
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__) + "/golden")
+    name, seed, B, L, Di, N = case
+    g = golden("scan.npz")
+    x, dt, Bm, Cm, A_log, D = scan_inputs(seed, B, L, Di, N)
+    A = (-np.exp(A_log)).astype(np.float32)
+    yp = R.parallel_scan(x, dt, A, Bm, Cm, D)
+    ys = R.sequential_scan(x, dt, A, Bm, Cm, D)
+    np.testing.assert_allclose(yp, g[name + "__parallel"], atol=5e-5, rtol=5e-5)
+    np.testing.assert_allclose(ys, g[name + "__sequential"], atol=5e-5, rtol=5e-5)
+    if L > 8:  # the reference's tree scan is NOT the recurrence
+        assert np.abs(g[name + "__parallel"] - g[name + "__sequential"]).max() > 1e-2
+
+
+def scan_inputs(seed, B, L, Di, N):
+    """Same draws as tests/golden/gen_goldens.py:scan_inputs."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B, L, Di)).astype(np.float32)
+    dt = np.log1p(np.exp(rng.standard_normal((B, L, Di)) * 0.7 - 1.0)).astype(np.float32)
+    Bm = rng.standard_normal((B, L, N)).astype(np.float32)
+    Cm = rng.standard_normal((B, L, N)).astype(np.float32)
+    A_log = (np.log(np.arange(1, N + 1)) + 0.01 * rng.standard_normal(N)).astype(np.float32)
+    D = (1.0 + 0.1 * rng.standard_normal(Di)).astype(np.float32)
+    return x, dt, Bm, Cm, A_log, D
+
+
+def test_forward_stages_b2_3s(default_weights):
+    g = golden("fwd_b2_3s.npz")
+    cfg = dict(S.DEFAULT_CONFIG)
+    mel = R.compute_mel_spectrogram(S.make_audio(2, 48000, seed=21))
+    np.testing.assert_allclose(mel, g["mel"], atol=2e-4, rtol=1e-4)
+    logits, f = R.forward(default_weights, g["mel"], cfg, return_features=True)
+    np.testing.assert_allclose(f["temporal_binding"], g["temporal_binding"], **FWD_TOL)
+    np.testing.assert_allclose(f["local_features"], g["local_features"], **FWD_TOL)
+    np.testing.assert_allclose(f["fused_features"], g["fused_features"], **FWD_TOL)
+    np.testing.assert_allclose(logits, g["logits"], **FWD_TOL)
+    np.testing.assert_array_equal(logits.argmax(-1), g["tokens"])
+
+
+def test_forward_from_audio_b2_3s(default_weights):
+    g = golden("fwd_b2_3s.npz")
+    mel = R.compute_mel_spectrogram(S.make_audio(2, 48000, seed=21))
+    logits = R.forward(default_weights, mel, dict(S.DEFAULT_CONFIG))
+    np.testing.assert_allclose(logits, g["logits"], atol=5e-4, rtol=1e-4)
+    np.testing.assert_array_equal(logits.argmax(-1), g["tokens"])
+    dec = golden_json("decode_fwd.json")["results"]
+    assert R.ctc_greedy_decode(logits) == dec["b2_3s"]
+    ts = R.ctc_greedy_decode_with_timestamps(logits)
+    assert [[t, [list(x) for x in s]] for t, s in ts] == dec["b2_3s_ts"]
+
+
+def test_forward_edge_lengths(default_weights):
+    g = golden("fwd_edge.npz")
+    for S_, seed in ((201, 31), (400, 32), (1600, 33), (8000, 34), (16333, 35)):
+        mel = R.compute_mel_spectrogram(S.make_audio(1, S_, seed=seed))
+        logits = R.forward(default_weights, mel, dict(S.DEFAULT_CONFIG))
+        np.testing.assert_allclose(logits, g[f"S{S_}__logits"], atol=5e-4, rtol=1e-4)
+        np.testing.assert_array_equal(logits.argmax(-1), g[f"S{S_}__tokens"])
+
+
+def test_forward_mel_input_500(default_weights):
+    g = golden("fwd_melin_500.npz")
+    mel = np.random.default_rng(41).standard_normal((2, 500, 80)).astype(np.float32)
+    logits = R.forward(default_weights, mel, dict(S.DEFAULT_CONFIG))
+    assert logits.shape == (2, 250, 1000)
+    np.testing.assert_allclose(logits, g["logits"], **FWD_TOL)
+    np.testing.assert_array_equal(logits.argmax(-1), g["tokens"])
+
+
+def test_forward_sequential_mode():
+    g = golden("fwd_seq_b2_3s.npz")
+    cfg = dict(S.DEFAULT_CONFIG, scan_mode="sequential")
+    W = S.make_weights(cfg, seed=0)
+    mel = R.compute_mel_spectrogram(S.make_audio(2, 48000, seed=21))
+    logits = R.forward(W, mel, cfg)
+    np.testing.assert_allclose(logits, g["logits"], atol=5e-4, rtol=1e-4)
+    np.testing.assert_array_equal(logits.argmax(-1), g["tokens"])
+
+
+def test_forward_small_config():
+    g = golden("fwd_smallcfg.npz")
+    cfg = dict(S.DEFAULT_CONFIG, **json.loads(str(g["meta"]))["config"])
+    W = S.make_weights(cfg, seed=3)
+    mel = R.compute_mel_spectrogram(S.make_audio(2, 32000, seed=51))
+    logits = R.forward(W, mel, cfg)
+    np.testing.assert_allclose(logits, g["logits"], atol=5e-4, rtol=1e-4)
+    np.testing.assert_array_equal(logits.argmax(-1), g["tokens"])
+
+
+@pytest.mark.slow
+def test_forward_10s_tokens(default_weights):
+    g = golden("fwd_b2_10s.npz")
+    mel = R.compute_mel_spectrogram(S.make_audio(2, 160000, seed=1234))
+    logits = R.forward(default_weights, mel, dict(S.DEFAULT_CONFIG))
+    np.testing.assert_array_equal(logits.argmax(-1), g["tokens"])
+    np.testing.assert_allclose(logits[:, g["frames"]], g["logits_sub"], atol=5e-4, rtol=1e-4)
+    assert R.ctc_greedy_decode(logits) == golden_json("decode_fwd.json")["results"]["b2_10s"]
+
+
+def test_decode_cases():
+    d = golden_json("decode.json")
+    for name, c in d["cases"].items():
+        lg = np.array(c["logits"], np.float32)
+        assert R.ctc_greedy_decode(lg) == c["greedy"], name
+        assert R.ctc_greedy_decode(lg, collapse_repeated=False) == c["greedy_nocollapse"], name
+        ts = R.ctc_greedy_decode_with_timestamps(lg)
+        assert [[t, [list(x) for x in s]] for t, s in ts] == c["timestamps"], name
