@@ -1,0 +1,177 @@
+/*
+ * vasr.h — C ABI of libvasr_hip.so, the MI355X (gfx950) kernels behind the
+ * VELOCITY-ASR inference path.
+ *
+ * The reference (shaderko/velocity-asr) has no native layer at all: its hot path is
+ * implicit ATen ops under Python modules.  Each entry point below replaces one of
+ * those op groups; the reference file:line it stands in for is cited per function.
+ * The one native-operator contract the reference itself defines is
+ * `selective_scan_fn(u, delta, A, B, C, D, z, ...)` (velocity_asr/ssm.py:20-26,
+ * call site ssm.py:326-332); vasr_ssm_scan_f32 is its replacement and also covers
+ * the reference's default pure-PyTorch tree scan (ssm.py:173-295).
+ *
+ * Conventions (all functions):
+ *   - All pointers are DEVICE pointers owned by the caller; the library never
+ *     allocates or frees on these paths (graph-capturable).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  Work is
+ *     enqueued, never synchronised.
+ *   - Matrices are row-major float32; `ld*` are row strides in ELEMENTS, `stride_*`
+ *     are batch strides in elements.
+ *   - Return 0 on success, a negative VASR_E* code for invalid arguments, or a
+ *     positive hipError_t if a launch failed.  vasr_last_error() returns a
+ *     thread-local description of the last failure.  No C++ exception crosses
+ *     this boundary.
+ *   - Functions are stateless and re-entrant.
+ */
+#ifndef VASR_H_
+#define VASR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VASR_ABI_VERSION 1
+
+#define VASR_OK 0
+#define VASR_EINVAL (-1)
+#define VASR_EUNSUPPORTED (-2)
+
+/* ABI version (== VASR_ABI_VERSION) and last-error text. */
+int vasr_version(void);
+const char* vasr_last_error(void);
+
+/* ------------------------------------------------------------------ GEMM
+ * C[b] = epilogue(A[b] (M x K) * W^T (K x N) + bias), W row-major [N][K] as in
+ * nn.Linear.  fp32 in / fp32 accumulate on v_mfma_f32_32x32x2f32.
+ * Replaces every nn.Linear / Conv1d-as-GEMM on the path: in_proj, x_proj+dt_proj
+ * (ssm.py:72-79, :105-113), out_proj (:90, :130), FFN (:394-400), temporal conv
+ * (model.py:156-162), pool_proj (attention.py:35, :76), q/k/v/out (:107-110),
+ * gated fusion (:183-218), CTC head (model.py:218-227), and the STFT as a
+ * windowed-DFT GEMM (audio.py:104-115).
+ */
+enum vasr_epilogue {
+    VASR_EPI_NONE = 0,          /* C = acc + bias                                      */
+    VASR_EPI_GELU = 1,          /* C = gelu_erf(acc + bias)                            */
+    VASR_EPI_SOFTPLUS_FROM = 2, /* C = acc + bias; softplus on columns >= n_out        */
+    VASR_EPI_RESIDUAL = 3,      /* C = (acc + bias) + aux[b][row][col]                 */
+    VASR_EPI_GELU_PE = 4,       /* C = gelu_erf(acc + bias) + aux[row][col] (pos. enc.) */
+    VASR_EPI_PAIR_POWER = 5,    /* W rows paired in 32s (re|im): C[row][k] = re^2+im^2 */
+    VASR_EPI_PAIR_FUSION = 6    /* W rows paired (gate|global): gated fusion, see doc  */
+};
+
+typedef struct vasr_gemm_args {
+    const float* A;
+    int64_t lda, stride_a;
+    const float* W;
+    int64_t ldw;
+    const float* bias;      /* [N] or NULL */
+    float* C;
+    int64_t ldc, stride_c;
+    int32_t batch, M, N, K; /* M rows per batch */
+    int32_t epilogue;       /* enum vasr_epilogue */
+    const float* aux;       /* residual / positional table / paired partial product */
+    int64_t ld_aux, stride_aux;
+    const float* aux2;      /* PAIR_FUSION: local_proj bias [n_out] */
+    int32_t n_out;          /* PAIR_*: output columns; SOFTPLUS_FROM: first softplus column */
+} vasr_gemm_args;
+
+int vasr_linear_f32(const vasr_gemm_args* args, void* stream);
+
+/* ------------------------------------------------------------------ norms / conv
+ * nn.LayerNorm over the last dim (C <= 1024), biased variance.  y may alias x.
+ * Replaces every LayerNorm on the path (26 per forward).
+ */
+int vasr_layer_norm_f32(const float* x, int64_t ldx, const float* w, const float* b,
+                        float* y, int64_t ldy, int rows, int C, float eps, void* stream);
+
+/* out[b][l][c] = x[b][l][c] + table[l][c] for x (B, L, C) contiguous (standalone
+ * PositionalEncoding2D.forward, model.py:106-127; the model fuses it into the conv GEMM). */
+int vasr_add_table_f32(const float* x, const float* table, float* out, int B, int L, int C,
+                       void* stream);
+
+/* SSMBlock pre-norm + causal depthwise conv (ssm.py:409-414, :377-383):
+ * y[b,t,c] = bias[c] + sum_j conv_w[c][j] * LN(x)[b, t-(Kc-1)+j, c]  (zero for t<0).
+ * x, y: (B, L, C) contiguous; conv_w: (C, Kc) contiguous; Kc <= 8.
+ */
+int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b,
+                       const float* conv_w, const float* conv_b, float* y,
+                       int B, int L, int C, int Kc, float eps, void* stream);
+
+/* ------------------------------------------------------------------ selective scan
+ * SelectiveSSM scan + D skip + SiLU gate (ssm.py:119-129):
+ *   dA = exp(dt*A), dBx = x*(dt*B)
+ *   mode 0 (scan_mode="parallel", the reference default): the reference's exclusive,
+ *          mis-combined Blelloch tree prefix h (ssm.py:216-295), streamed in its exact
+ *          float-operation order with an O(log L) block stack per state lane;
+ *   mode 1 (scan_mode="sequential"): the true recurrence h_t = dA_t h_{t-1} + dBx_t
+ *          (ssm.py:134-171);
+ *   out[b,t,d] = (sum_n h[b,t,d,n] C[b,t,n] + x[b,t,d] D[d]) * silu(z[b,t,d]).
+ * x = xz[:, :, 0:Di], z = xz[:, :, Di:2Di]; B = bc[:, :, 0:N], C = bc[:, :, N:2N].
+ * A2 = A * log2(e) (A = -exp(A_log), shared across Di).  N in {16, 32, 64};
+ * Di % (4096/N) == 0 for N = 64 ... (host checks); L <= 8192.
+ */
+int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,
+                      const float* bc, int64_t ld_bc, const float* A2, const float* D,
+                      float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
+                      void* stream);
+
+/* ------------------------------------------------------------------ mel front end
+ * compute_mel_spectrogram (audio.py:65-143) is three launches:
+ *  1. vasr_reflect_pad_f32: xp[b][0:S+2*pad] = reflect-padded audio (audio.py:100-101),
+ *     rows of stride ld_out (>= S + 2*pad + n_fft); the tail is zero-filled.
+ *  2. vasr_linear_f32 with VASR_EPI_PAIR_POWER on rows of stride `hop` of xp against the
+ *     Hann-windowed DFT matrix -> power[b][f][k] = |X_k|^2 (audio.py:104-115).
+ *  3. vasr_mel_log_norm_f32: mel = fb @ power (audio.py:126), log(mel + 1e-10) (:129),
+ *     per-(b, mel bin) (x - mean)/(std_unbiased + 1e-10) over frames (:132-135), written
+ *     to out[b][frame_off + f][m] with batch stride out_stride (frames of a padded
+ *     layout are left untouched).  fb is passed in CSR form (rows = mel bins).
+ */
+int vasr_reflect_pad_f32(const float* audio, int64_t ld_audio, float* xp, int64_t ld_out,
+                         int B, int S, int pad, void* stream);
+int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t stride_power,
+                          const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
+                          float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
+                          int normalize, float* workspace, void* stream);
+
+/* Write (B, F, C) rows into a zero-padded frame layout: out[b][off + f][c] = x[b][f][c]
+ * and zero for the other out_frames - F frames (batch stride out_frames * C).  Feeds mel
+ * to the stride-2 temporal conv, whose im2col rows are then plain strided rows. */
+int vasr_pad_frames_f32(const float* x, float* out, int out_frames, int off,
+                        int B, int F, int C, void* stream);
+
+/* ------------------------------------------------------------------ global context
+ * F.adaptive_avg_pool1d over time (attention.py:71-73): bin i = [floor(iL/K), ceil((i+1)L/K)).
+ * x: (B, L, C), out: (B, K, C).
+ */
+int vasr_adaptive_pool_f32(const float* x, float* out, int B, int L, int C, int K, void* stream);
+
+/* Pooled multi-head cross attention core (attention.py:143-160), no mask:
+ * out[b,t,h*hd:(h+1)*hd] = softmax(q_bth . k_bh^T / sqrt(hd)) v_bh over the Kp pooled keys.
+ * q: (B, L, A) with row stride ld_q; kv: (B, Kp, 2A) [k | v]; out: (B, L, A) contiguous.
+ * Kp <= 64, hd <= 64.
+ */
+int vasr_pooled_attention_f32(const float* q, int64_t ld_q, const float* kv, float* out,
+                              int B, int L, int Kp, int heads, int head_dim, void* stream);
+
+/* ------------------------------------------------------------------ CTC decode
+ * argmax over V per row, ties -> first index (decode.py:46).
+ */
+int vasr_argmax_f32(const float* logits, int64_t ld, int rows, int V, int32_t* out, void* stream);
+
+/* Greedy CTC collapse per utterance (decode.py:51-69, :89-123): drop blank (and reset
+ * prev), skip repeats of prev if collapse != 0.  out_tokens (B, L) holds each
+ * utterance's kept tokens left-aligned, out_len (B) their counts.  If out_start /
+ * out_end are non-NULL they receive the (start_frame, end_frame) of each kept token
+ * with the semantics of ctc_greedy_decode_with_timestamps (collapse must be 1).
+ */
+int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse,
+                      int32_t* out_tokens, int32_t* out_len, int32_t* out_start,
+                      int32_t* out_end, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VASR_H_ */

@@ -1,0 +1,168 @@
+"""CPU-side tests: C ABI exports, module/state_dict contract, checkpoint format, host logic.
+
+No kernel is launched here (there is no GPU in the build container); the GPU parity
+tests are in test_gpu_parity.py (pytest -m gpu).
+"""
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, golden_json
+from velocity_asr import synthetic as S
+
+
+def test_c_abi_library_exports_every_header_symbol():
+    from velocity_asr import _lib
+    names = _lib.header_functions()
+    assert "vasr_ssm_scan_f32" in names and "vasr_linear_f32" in names
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert lib.vasr_version() == _lib.ABI_VERSION
+    # every declared symbol has a typed binding
+    assert set(names) <= set(_lib._SIGNATURES)
+
+
+def test_abi_rejects_bad_arguments_without_gpu():
+    """Argument validation happens before any launch, so it is testable on the host."""
+    from velocity_asr import _lib
+    L = _lib.load()
+    rc = L.vasr_ssm_scan_f32(None, 0, None, 0, None, 0, None, None, None, 0, 1, 1, 384, 64, 0, None)
+    assert rc == -1 and b"null" in L.vasr_last_error()
+    rc = L.vasr_ctc_collapse(None, 1, 1, 0, 1, None, None, None, None, None)
+    assert rc == -1
+    args = _lib.GemmArgs()
+    assert L.vasr_linear_f32(ctypes.byref(args), None) == -1
+
+
+def test_public_api_matches_reference_all():
+    import velocity_asr as v
+    expected = {"VELOCITYASR", "VelocityASRConfig", "from_pretrained", "TemporalBindingLayer", "CTCOutputHead",
+                "SelectiveSSM", "SSMBlock", "LocalSSMProcessor", "GlobalSSM", "ScanMode", "MAMBA_AVAILABLE",
+                "HierarchicalGlobalContext", "AdaptivePool", "MultiHeadAttention", "GatedFusion", "load_audio",
+                "compute_mel_spectrogram", "MelSpectrogramTransform", "audio_to_frames", "frames_to_audio",
+                "pad_or_trim", "SAMPLE_RATE", "N_FFT", "HOP_LENGTH", "N_MELS", "ctc_greedy_decode",
+                "ctc_greedy_decode_with_timestamps", "ctc_beam_search", "CTCDecoder", "DecodingResult",
+                "create_default_vocabulary", "ASRDataset", "ASRCollator", "LibriSpeechDataset",
+                "create_dataloader", "create_librispeech_dataloaders", "__version__", "__author__"}
+    assert expected == set(v.__all__)
+    for n in expected:
+        assert hasattr(v, n), n
+    from velocity_asr.audio import SAMPLE_RATE, HOP_LENGTH  # scripts/transcribe.py:33
+    from velocity_asr.training import compute_wer, compute_cer  # scripts/evaluate.py:31
+    assert (SAMPLE_RATE, HOP_LENGTH) == (16000, 160)
+
+
+@pytest.mark.parametrize("cfg", [None, dict(d_model=96, ssm_layers=2, ssm_state_dim=32, global_ssm_state_dim=16,
+                                            attention_heads=2, attention_dim=24, vocab_size=50)])
+def test_state_dict_contract(cfg):
+    import velocity_asr as v
+    m = v.VELOCITYASR(v.VelocityASRConfig(**(cfg or {})))
+    spec = S.state_dict_spec(cfg)
+    sd = m.state_dict()
+    assert [k for k, _, _ in spec] == list(sd.keys())
+    assert all(tuple(sd[k].shape) == s for k, s, _ in spec)
+    if cfg is None:
+        assert len(sd) == 208 and m.count_parameters() == 6_172_696
+
+
+def test_checkpoint_roundtrip_and_strict_load(tmp_path):
+    import velocity_asr as v
+    m = v.VELOCITYASR()
+    W = S.make_weights(None, seed=0)
+    m.load_state_dict({k: torch.from_numpy(a) for k, a in W.items()}, strict=True)
+    path = str(tmp_path / "ck" / "model.pt")
+    m.save_pretrained(path)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert set(ck) == {"config", "model_state_dict"} and len(ck["config"]) == 15
+    m2 = v.from_pretrained(path)
+    for k, a in m2.state_dict().items():
+        assert torch.equal(a, m.state_dict()[k]), k
+    # Trainer-style checkpoint: 'config' holds the training config -> default model config
+    torch.save({"model_state_dict": m.state_dict(), "config": {"learning_rate": 1e-3}}, str(tmp_path / "t.pt"))
+    assert v.VELOCITYASR.from_pretrained(str(tmp_path / "t.pt")).config == v.VelocityASRConfig()
+    with pytest.raises(NotImplementedError):
+        v.VELOCITYASR.from_pretrained("velocity-asr-v2")
+
+
+def test_config_from_dict_filters_unknown_keys():
+    import velocity_asr as v
+    c = v.VelocityASRConfig.from_dict({"d_model": 96, "bogus": 1, "scan_mode": "sequential"})
+    assert c.d_model == 96 and c.scan_mode == "sequential"
+
+
+def test_seeded_init_is_the_reference_init():
+    """torch.manual_seed(s); VELOCITYASR() draws the same numbers as the reference
+    (same module order and initialisers, model.py:305-318)."""
+    import velocity_asr as v
+    torch.manual_seed(0)
+    a = v.VELOCITYASR().state_dict()
+    torch.manual_seed(0)
+    b = v.VELOCITYASR().state_dict()
+    assert all(torch.equal(a[k], b[k]) for k in a)
+    # init statistics of the reference initialiser
+    assert torch.all(a["local_ssm.layers.0.ssm.D"] == 1)
+    assert torch.allclose(a["local_ssm.layers.0.ssm.A_log"], torch.log(torch.arange(1, 65.0)))
+    assert torch.all(a["ctc_head.proj.2.bias"] == 0)
+
+
+def test_vocabulary_and_text():
+    import velocity_asr as v
+    d = golden_json("decode.json")
+    vocab = v.create_default_vocabulary(1000)
+    assert len(vocab) == d["vocab_len"] and vocab[:80] == d["vocab_head"] and vocab[-3:] == d["vocab_tail"]
+    assert v.create_default_vocabulary(10) == d["vocab_small"]
+    dec = v.CTCDecoder(vocab)
+    assert dec._tokens_to_text([30, 4, 3, 5, 9999]) == "Aa b<unk>"
+    assert dec.text_to_tokens("ab") == [4, 5]
+
+
+def test_wer_cer_match_reference():
+    from velocity_asr.training import compute_cer, compute_wer
+    for c in golden_json("decode.json")["wer"]:
+        assert compute_wer(c["pred"], c["ref"]) == pytest.approx(c["wer"], abs=0)
+        assert compute_cer(c["pred"], c["ref"]) == pytest.approx(c["cer"], abs=0)
+
+
+def test_audio_helpers_and_wav_reader(tmp_path):
+    import wave
+    import velocity_asr as v
+    assert v.audio_to_frames(160000) == 1002  # reference off-by-one kept (audio.py:280)
+    assert v.frames_to_audio(10) == 1600
+    x = torch.arange(10.0)
+    assert v.pad_or_trim(x, 4).tolist() == [0, 1, 2, 3]
+    assert v.pad_or_trim(x, 12)[-2:].tolist() == [0, 0]
+    sig = (np.sin(np.arange(1600) / 7.0) * 12000).astype("<i2")
+    p = str(tmp_path / "a.wav")
+    with wave.open(p, "wb") as w:
+        w.setnchannels(2)
+        w.setsampwidth(2)
+        w.setframerate(16000)
+        w.writeframes(np.stack([sig, sig // 2], 1).tobytes())
+    a = v.load_audio(p)
+    assert a.shape == (1600,) and a.dtype == torch.float32
+    np.testing.assert_allclose(a.numpy(), (sig.astype(np.float32) + (sig // 2).astype(np.float32)) / 2 / 32768, atol=1e-6)
+    assert v.load_audio(p, mono=False).shape == (2, 1600)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU error path")
+def test_no_cpu_fallback():
+    import velocity_asr as v
+    m = v.VELOCITYASR().eval()
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(torch.randn(1, 50, 80))
+    with pytest.raises(RuntimeError, match="HIP device"):
+        v.compute_mel_spectrogram(torch.randn(16000))
+    with pytest.raises(RuntimeError, match="HIP device"):
+        v.ctc_greedy_decode(torch.randn(1, 5, 10))
+
+
+def test_mamba_mode_and_bad_mode():
+    import velocity_asr as v
+    v.SelectiveSSM(scan_mode="mamba")  # served by the HIP recurrence kernel
+    with pytest.raises(ValueError):
+        v.SelectiveSSM(scan_mode="bogus")

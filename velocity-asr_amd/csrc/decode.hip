@@ -1,0 +1,92 @@
+// CTC greedy decode on device (reference velocity_asr/decode.py:27-125).
+//  argmax   : one wave per frame row over V logits, ties -> lowest index (torch.argmax).
+//  collapse : per utterance, keep each maximal run of one non-blank token once
+//             (collapse=1; decode.py:56-67) or every non-blank frame (collapse=0), and
+//             optionally the run's [start, end) frames (with_timestamps, decode.py:89-123).
+#include "vasr_internal.h"
+
+namespace vasr {
+namespace {
+
+__global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ x, int64_t ld, int rows, int V,
+                                                     int32_t* __restrict__ out) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const float* xr = x + (int64_t)row * ld;
+    float best = -INFINITY;
+    int bi = V;  // sentinel larger than any index
+    for (int j = lane; j < V; j += 64) {
+        const float v = xr[j];
+        // NaN propagates as the max (torch semantics); first index wins ties
+        if (v > best || (v != v && best == best)) {
+            best = v;
+            bi = j;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        const bool o_nan = ov != ov, b_nan = best != best;
+        bool take;
+        if (o_nan || b_nan) take = o_nan && (!b_nan || oi < bi);
+        else take = ov > best || (ov == best && oi < bi);
+        if (take) {
+            best = ov;
+            bi = oi;
+        }
+    }
+    if (lane == 0) out[row] = bi < V ? bi : 0;
+}
+
+__global__ void collapse_kernel(const int32_t* __restrict__ pred, int B, int L, int blank, int collapse,
+                                int32_t* __restrict__ toks, int32_t* __restrict__ lens, int32_t* __restrict__ st,
+                                int32_t* __restrict__ en) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int32_t* p = pred + (int64_t)b * L;
+    int32_t* o = toks + (int64_t)b * L;
+    int n = 0;
+    int prev = -1;  // "None"
+    for (int t = 0; t < L; ++t) {
+        const int tok = p[t];
+        if (tok == blank) {
+            if (st && prev != -1 && prev != blank) en[(int64_t)b * L + n - 1] = t;
+            prev = st ? tok : -1;
+            continue;
+        }
+        if (collapse && tok == prev) continue;
+        if (st && prev != -1 && prev != blank) en[(int64_t)b * L + n - 1] = t;
+        if (st) st[(int64_t)b * L + n] = t;
+        o[n++] = tok;
+        prev = tok;
+    }
+    if (st && prev != -1 && prev != blank) en[(int64_t)b * L + n - 1] = L;
+    lens[b] = n;
+}
+
+}  // namespace
+}  // namespace vasr
+
+VASR_API int vasr_argmax_f32(const float* logits, int64_t ld, int rows, int V, int32_t* out, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(logits && out, "vasr_argmax_f32: null pointer");
+    VASR_CHECK_ARG(rows >= 0 && V >= 1 && ld >= V, "vasr_argmax_f32: bad shape");
+    if (rows == 0) return VASR_OK;
+    hipLaunchKernelGGL(argmax_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), logits, ld, rows, V, out);
+    return launch_status("vasr_argmax_f32");
+}
+
+VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse, int32_t* out_tokens,
+                               int32_t* out_len, int32_t* out_start, int32_t* out_end, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(pred && out_tokens && out_len, "vasr_ctc_collapse: null pointer");
+    VASR_CHECK_ARG((out_start == nullptr) == (out_end == nullptr), "vasr_ctc_collapse: start/end must both be set");
+    VASR_CHECK_ARG(out_start == nullptr || collapse, "vasr_ctc_collapse: timestamps need collapse=1");
+    VASR_CHECK_ARG(B >= 0 && L >= 0, "vasr_ctc_collapse: bad shape");
+    if (B == 0) return VASR_OK;
+    hipLaunchKernelGGL(collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, as_stream(stream), pred, B, L, blank, collapse,
+                       out_tokens, out_len, out_start, out_end);
+    return launch_status("vasr_ctc_collapse");
+}

@@ -1,0 +1,131 @@
+// LayerNorm and the SSMBlock pre-norm + causal depthwise conv.
+//
+// Both are HBM-bound row kernels: one wave per 192-float token row, three floats per
+// lane, statistics by wave butterfly (no LDS round trip).  The fused LN+dwconv tile
+// normalises TT + Kc - 1 rows (the Kc - 1 history rows of the causal window are
+// recomputed, not re-read) into LDS and emits TT output rows.
+#include "vasr_internal.h"
+
+namespace vasr {
+namespace {
+
+constexpr int kMaxPerLane = 16;  // C <= 1024
+
+__device__ __forceinline__ void ln_row_to(const float* __restrict__ x, const float* __restrict__ w,
+                                          const float* __restrict__ b, float* __restrict__ y, int C,
+                                          float eps, int lane) {
+    float v[kMaxPerLane];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxPerLane; ++i) {
+        const int c = i * 64 + lane;
+        v[i] = (c < C) ? x[c] : 0.f;
+        s += v[i];
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxPerLane; ++i) {
+        const int c = i * 64 + lane;
+        const float d = (c < C) ? v[i] - mean : 0.f;
+        q += d * d;
+    }
+    const float var = wave_sum(q) / (float)C;
+    const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+    for (int i = 0; i < kMaxPerLane; ++i) {
+        const int c = i * 64 + lane;
+        if (c < C) y[c] = (v[i] - mean) * rstd * w[c] + b[c];
+    }
+}
+
+__global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict__ x, int64_t ldx,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ b, float* y,
+                                                         int64_t ldy, int rows, int C, float eps) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    ln_row_to(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
+}
+
+constexpr int TT = 32;       // output rows per block
+constexpr int kMaxC = 256;   // LDS row capacity
+constexpr int kMaxK = 8;
+
+__global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ ln_w,
+                                                        const float* __restrict__ ln_b,
+                                                        const float* __restrict__ cw,
+                                                        const float* __restrict__ cb, float* __restrict__ y,
+                                                        int L, int C, int Kc, float eps) {
+    __shared__ float tile[(TT + kMaxK - 1) * kMaxC];
+    const int b = blockIdx.y;
+    const int t0 = blockIdx.x * TT;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nrows = TT + Kc - 1;
+    const float* xb = x + (int64_t)b * L * C;
+    for (int rr = wave; rr < nrows; rr += 4) {
+        const int t = t0 - (Kc - 1) + rr;
+        float* dst = tile + rr * kMaxC;
+        if (t < 0 || t >= L) {
+            for (int c = lane; c < C; c += 64) dst[c] = 0.f;  // causal zero padding
+        } else {
+            ln_row_to(xb + (int64_t)t * C, ln_w, ln_b, dst, C, eps, lane);
+        }
+    }
+    __syncthreads();
+    float* yb = y + (int64_t)b * L * C;
+    for (int idx = threadIdx.x; idx < TT * C; idx += 256) {
+        const int tt = idx / C, c = idx - tt * C;
+        const int t = t0 + tt;
+        if (t >= L) break;
+        float acc = 0.f;
+        for (int j = 0; j < Kc; ++j) acc += tile[(tt + j) * kMaxC + c] * cw[c * Kc + j];
+        yb[(int64_t)t * C + c] = acc + cb[c];
+    }
+}
+
+__global__ void add_table_kernel(const float* __restrict__ x, const float* __restrict__ table, float* __restrict__ out,
+                                 int64_t n, int64_t per_batch) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = x[i] + table[i % per_batch];
+}
+
+}  // namespace
+}  // namespace vasr
+
+VASR_API int vasr_add_table_f32(const float* x, const float* table, float* out, int B, int L, int C, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && table && out && B >= 0 && L >= 0 && C >= 0, "vasr_add_table_f32: bad arguments");
+    const int64_t n = (int64_t)B * L * C;
+    if (n == 0) return VASR_OK;
+    const int blocks = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+    hipLaunchKernelGGL(add_table_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, table, out, n,
+                       (int64_t)L * C);
+    return launch_status("vasr_add_table_f32");
+}
+
+VASR_API int vasr_layer_norm_f32(const float* x, int64_t ldx, const float* w, const float* b, float* y,
+                                 int64_t ldy, int rows, int C, float eps, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && w && b && y, "vasr_layer_norm_f32: null pointer");
+    VASR_CHECK_ARG(C > 0 && C <= 64 * kMaxPerLane && rows >= 0, "vasr_layer_norm_f32: bad shape rows=%d C=%d", rows, C);
+    if (rows == 0) return VASR_OK;
+    hipLaunchKernelGGL(layer_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, ldx, w, b, y,
+                       ldy, rows, C, eps);
+    return launch_status("vasr_layer_norm_f32");
+}
+
+VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b, const float* conv_w,
+                                const float* conv_b, float* y, int B, int L, int C, int Kc, float eps,
+                                void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && ln_w && ln_b && conv_w && conv_b && y, "vasr_ln_dwconv_f32: null pointer");
+    VASR_CHECK_ARG(x != y, "vasr_ln_dwconv_f32: in-place not supported");
+    VASR_CHECK_ARG(C > 0 && C <= kMaxC && Kc >= 1 && Kc <= kMaxK && B >= 0 && L >= 0,
+                   "vasr_ln_dwconv_f32: unsupported shape C=%d Kc=%d", C, Kc);
+    if (B == 0 || L == 0) return VASR_OK;
+    hipLaunchKernelGGL(ln_dwconv_kernel, dim3((L + TT - 1) / TT, B), dim3(256), 0, as_stream(stream), x, ln_w,
+                       ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+    return launch_status("vasr_ln_dwconv_f32");
+}

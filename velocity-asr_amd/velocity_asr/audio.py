@@ -1,0 +1,228 @@
+"""Audio loading and the log-mel front end (drop-in for reference velocity_asr/audio.py).
+
+compute_mel_spectrogram runs on the MI355X: reflect pad (HIP) -> windowed-DFT GEMM with
+an in-register |X|^2 epilogue (fp32 MFMA) -> sparse mel + log + per-bin normalisation
+(HIP).  Input on the CPU is moved to the current HIP device and the result moved back,
+so callers that compute mel on the host (scripts/transcribe.py:73) keep working; there is
+no CPU execution path.
+
+Constant tables (Hann window, mel filterbank) are built once per device with the
+reference's own float32 formulas (audio.py:97, :146-199), so they are bit-identical to
+what the reference uses.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import wave
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from . import ops
+
+# Default audio parameters (reference audio.py:15-19)
+SAMPLE_RATE = 16000
+N_FFT = 400
+HOP_LENGTH = 160
+N_MELS = 80
+WINDOW_FN = torch.hann_window
+
+
+def _read_wav(path: str) -> Tuple[torch.Tensor, int]:
+    """PCM WAV reader (stdlib wave): (channels, samples) float32 in [-1, 1), like torchaudio.load."""
+    with wave.open(path, "rb") as w:
+        nch, width, sr, n = w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()
+        raw = w.readframes(n)
+    if width == 1:
+        x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
+    elif width == 2:
+        x = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
+    elif width == 3:
+        b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
+        v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        x = v.astype(np.float32) / float(1 << 23)
+    elif width == 4:
+        x = np.frombuffer(raw, "<i4").astype(np.float32) / float(1 << 31)
+    else:
+        raise ValueError(f"unsupported WAV sample width {width}")
+    return torch.from_numpy(np.ascontiguousarray(x.reshape(-1, nch).T)), sr
+
+
+def load_audio(path: str, sample_rate: int = SAMPLE_RATE, mono: bool = True) -> torch.Tensor:
+    """Load audio and resample (reference audio.py:22-62).
+
+    Uses torchaudio when it is installed (same as the reference); otherwise reads PCM WAV
+    with the standard library.  Returns (samples,) for mono or (channels, samples).
+    """
+    try:
+        import torchaudio  # noqa: F401
+        waveform, sr = torchaudio.load(path)
+    except ImportError:
+        if not path.lower().endswith(".wav"):
+            raise ImportError("torchaudio is required for non-WAV audio. Install with: pip install torchaudio")
+        waveform, sr = _read_wav(path)
+    if mono and waveform.size(0) > 1:
+        waveform = waveform.mean(dim=0, keepdim=True)
+    if sr != sample_rate:
+        try:
+            import torchaudio
+        except ImportError:
+            raise ImportError(f"resampling {sr} Hz -> {sample_rate} Hz needs torchaudio")
+        waveform = torchaudio.transforms.Resample(sr, sample_rate)(waveform)
+    if mono:
+        waveform = waveform.squeeze(0)
+    return waveform
+
+
+def _create_mel_filterbank(n_fft: int, n_mels: int, sample_rate: int, device: torch.device) -> torch.Tensor:
+    """HTK triangular filterbank, float32 torch ops in the reference's order (audio.py:146-199).
+    Built once per configuration on the host; it is a constant table of the front end."""
+    n_freqs = n_fft // 2 + 1
+    freqs = torch.linspace(0, sample_rate / 2, n_freqs)
+
+    def hz_to_mel(hz):
+        return 2595 * torch.log10(1 + hz / 700)
+
+    def mel_to_hz(mel):
+        return 700 * (10 ** (mel / 2595) - 1)
+
+    mel_min = hz_to_mel(torch.tensor(0.0))
+    mel_max = hz_to_mel(torch.tensor(sample_rate / 2.0))
+    mel_points = torch.linspace(mel_min, mel_max, n_mels + 2)
+    hz_points = mel_to_hz(mel_points)
+    fb = torch.zeros(n_mels, n_freqs)
+    for i in range(n_mels):
+        lower, center, upper = hz_points[i], hz_points[i + 1], hz_points[i + 2]
+        lower_slope = (freqs - lower) / (center - lower + 1e-10)
+        upper_slope = (upper - freqs) / (upper - center + 1e-10)
+        fb[i] = torch.maximum(torch.zeros_like(freqs), torch.minimum(lower_slope, upper_slope))
+    return fb.to(device)
+
+
+class _FrontEndTables:
+    """Per (device, n_fft, n_mels, sample_rate) constants: paired DFT matrix and CSR filterbank."""
+
+    def __init__(self, device: torch.device, n_fft: int, n_mels: int, sample_rate: int):
+        n_bins = n_fft // 2 + 1
+        pairs = (n_bins + 31) // 32
+        win = WINDOW_FN(n_fft).double().numpy()          # reference window, float32 values
+        n = np.arange(n_fft, dtype=np.float64)
+        W = np.zeros((pairs * 64, n_fft), dtype=np.float64)
+        for k in range(n_bins):
+            p, j = divmod(k, 32)
+            ang = 2.0 * math.pi * ((k * n) % n_fft) / n_fft
+            W[64 * p + j] = win * np.cos(ang)
+            W[64 * p + 32 + j] = -win * np.sin(ang)
+        self.n_bins = n_bins
+        self.dft = torch.from_numpy(W.astype(np.float32)).to(device)
+        fb = _create_mel_filterbank(n_fft, n_mels, sample_rate, torch.device("cpu"))
+        nz = fb.nonzero(as_tuple=False)
+        rowptr = torch.zeros(n_mels + 1, dtype=torch.int32)
+        counts = torch.bincount(nz[:, 0], minlength=n_mels)
+        rowptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        self.fb_csr = (rowptr.to(device), nz[:, 1].to(torch.int32).contiguous().to(device),
+                       fb[nz[:, 0], nz[:, 1]].contiguous().to(device))
+
+
+_TABLES: Dict[tuple, _FrontEndTables] = {}
+
+
+def _tables(device: torch.device, n_fft: int, n_mels: int, sample_rate: int) -> _FrontEndTables:
+    key = (str(device), n_fft, n_mels, sample_rate)
+    t = _TABLES.get(key)
+    if t is None:
+        t = _TABLES[key] = _FrontEndTables(device, n_fft, n_mels, sample_rate)
+    return t
+
+
+def _target_device(t: torch.Tensor) -> torch.device:
+    if t.device.type == "cuda":
+        return t.device
+    _lib.require_device()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def compute_mel_spectrogram(audio: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
+                            hop_length: int = HOP_LENGTH, n_mels: int = N_MELS,
+                            normalize: bool = True) -> torch.Tensor:
+    """Log-mel spectrogram (reference audio.py:65-143) on the MI355X.
+
+    audio (samples,) or (batch, samples) -> (frames, n_mels) or (batch, frames, n_mels),
+    frames = samples // hop_length + 1, on the input's device.
+    """
+    squeeze = audio.dim() == 1
+    if squeeze:
+        audio = audio.unsqueeze(0)
+    if audio.dim() != 2:
+        raise ValueError(f"compute_mel_spectrogram: expected (samples,) or (batch, samples), got {tuple(audio.shape)}")
+    dev = _target_device(audio)
+    x = audio.to(device=dev, dtype=torch.float32).contiguous()
+    mel = mel_on_device(x, sample_rate, n_fft, hop_length, n_mels, normalize)
+    if audio.device.type != "cuda":
+        mel = mel.to(audio.device)
+    return mel.squeeze(0) if squeeze else mel
+
+
+def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
+                  hop_length: int = HOP_LENGTH, n_mels: int = N_MELS, normalize: bool = True) -> torch.Tensor:
+    """(B, S) float32 HIP tensor -> (B, F, n_mels) on the same device."""
+    B, S = x.shape
+    pad = n_fft // 2
+    if S <= pad:
+        raise RuntimeError(f"compute_mel_spectrogram: reflect padding of {pad} needs more than {pad} samples, got {S}")
+    if n_fft % 4 or hop_length % 4:
+        raise NotImplementedError("HIP front end needs n_fft and hop_length to be multiples of 4")
+    n_frames = (S + 2 * pad - n_fft) // hop_length + 1
+    tb = _tables(x.device, n_fft, n_mels, sample_rate)
+    ld = (S + 2 * pad + 3) // 4 * 4
+    xp = ops.reflect_pad(x, pad, ld)
+    power = torch.empty((B, n_frames, tb.n_bins), device=x.device, dtype=torch.float32)
+    ops.gemm_batched(xp, hop_length, ld, n_frames, B, n_fft, tb.dft, None, power, tb.n_bins, n_frames * tb.n_bins,
+                     epilogue=_lib.EPI_PAIR_POWER, n_out=tb.n_bins)
+    return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize)
+
+
+class MelSpectrogramTransform(nn.Module):
+    """nn.Module wrapper of compute_mel_spectrogram (reference audio.py:202-261); same buffers."""
+
+    def __init__(self, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT, hop_length: int = HOP_LENGTH,
+                 n_mels: int = N_MELS, normalize: bool = True):
+        super().__init__()
+        self.sample_rate = sample_rate
+        self.n_fft = n_fft
+        self.hop_length = hop_length
+        self.n_mels = n_mels
+        self.normalize = normalize
+        self.register_buffer("window", WINDOW_FN(n_fft))
+        self.register_buffer("mel_filters", _create_mel_filterbank(n_fft, n_mels, sample_rate, torch.device("cpu")))
+
+    def forward(self, audio: torch.Tensor) -> torch.Tensor:
+        return compute_mel_spectrogram(audio, sample_rate=self.sample_rate, n_fft=self.n_fft,
+                                       hop_length=self.hop_length, n_mels=self.n_mels, normalize=self.normalize)
+
+
+def audio_to_frames(audio_length: int, hop_length: int = HOP_LENGTH, n_fft: int = N_FFT) -> int:
+    """Same formula as the reference (audio.py:264-280), including its off-by-one:
+    compute_mel_spectrogram produces audio_length // hop_length + 1 frames."""
+    return (audio_length + n_fft) // hop_length
+
+
+def frames_to_audio(num_frames: int, hop_length: int = HOP_LENGTH) -> int:
+    return num_frames * hop_length
+
+
+def pad_or_trim(audio: torch.Tensor, target_length: int) -> torch.Tensor:
+    """Zero-pad or trim the last dim to target_length (reference audio.py:300-324)."""
+    current = audio.shape[-1]
+    if current > target_length:
+        return audio[..., :target_length]
+    if current < target_length:
+        return F.pad(audio, (0, target_length - current))
+    return audio

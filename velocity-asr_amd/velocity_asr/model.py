@@ -1,0 +1,232 @@
+"""VELOCITY-ASR model (drop-in for reference velocity_asr/model.py) on MI355X kernels.
+
+Module tree, parameter/buffer names, config dataclass and checkpoint format are the
+reference's (model.py:23-467), so reference checkpoints load with strict=True and
+scripts/transcribe.py / scripts/evaluate.py work unchanged.  The forward pass runs
+entirely in libvasr_hip.so; CPU tensors are rejected with a clear error.
+"""
+
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib, ops
+from ._prep import cached
+from .attention import HierarchicalGlobalContext
+from .ssm import LocalSSMProcessor, ScanMode
+
+
+@dataclass
+class VelocityASRConfig:
+    """Configuration for VELOCITY-ASR (reference model.py:23-68)."""
+
+    mel_bins: int = 80
+    d_model: int = 192
+    ssm_layers: int = 8
+    ssm_state_dim: int = 64
+    ssm_expand_ratio: int = 2
+    ssm_kernel_size: int = 4
+    global_ssm_layers: int = 2
+    global_ssm_state_dim: int = 32
+    attention_heads: int = 4
+    attention_dim: int = 48
+    vocab_size: int = 1000
+    dropout: float = 0.1
+    gradient_checkpointing: bool = False
+    scan_mode: ScanMode = "parallel"
+    use_compile: bool = False
+
+    @classmethod
+    def from_dict(cls, config_dict: Dict[str, Any]) -> "VelocityASRConfig":
+        return cls(**{k: v for k, v in config_dict.items() if k in cls.__dataclass_fields__})
+
+
+class PositionalEncoding2D(nn.Module):
+    """[sinusoidal time (D/2) | learned frequency (D/2)] encoding (reference model.py:71-127)."""
+
+    def __init__(self, d_model: int = 192, max_len: int = 5000, mel_bins: int = 80):
+        super().__init__()
+        self.d_model = d_model
+        pe_time = torch.zeros(max_len, d_model // 2)
+        position = torch.arange(0, max_len, dtype=torch.float).unsqueeze(1)
+        div_term = torch.exp(torch.arange(0, d_model // 2, 2).float() * (-math.log(10000.0) / (d_model // 2)))
+        pe_time[:, 0::2] = torch.sin(position * div_term)
+        pe_time[:, 1::2] = torch.cos(position * div_term)
+        self.register_buffer("pe_time", pe_time)
+        self.pe_freq = nn.Parameter(torch.randn(1, 1, d_model // 2) * 0.02)
+
+    def table(self, seq_len: int) -> torch.Tensor:
+        """(seq_len, d_model) rows [pe_time[t] | pe_freq] on the parameters' device."""
+        if seq_len > self.pe_time.shape[0]:
+            raise RuntimeError(f"sequence of {seq_len} tokens exceeds the positional table ({self.pe_time.shape[0]}); "
+                               "the reference fails the same way (model.py:125)")
+
+        def build():
+            half = self.pe_time.shape[1]
+            return torch.cat([self.pe_time[:seq_len], self.pe_freq.reshape(1, half).expand(seq_len, half)],
+                             -1).contiguous()
+        return cached(self, f"pe{seq_len}", (self.pe_time, self.pe_freq), build)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, L, D = x.shape
+        return ops.add_table(x, self.table(L))
+
+
+class TemporalBindingLayer(nn.Module):
+    """Conv1d(k3, s2) -> GELU -> +2-D PE -> LayerNorm (reference model.py:130-202).
+
+    One batched fp32-MFMA GEMM: the mel frames are zero-padded once so every conv output
+    row is a plain strided row (stride 2 frames, K = 3 frames) of the padded buffer; bias,
+    exact GELU and the positional table are fused in the epilogue.
+    """
+
+    def __init__(self, mel_bins: int = 80, d_model: int = 192, kernel_size: int = 3, stride: int = 2):
+        super().__init__()
+        self.conv = nn.Conv1d(in_channels=mel_bins, out_channels=d_model, kernel_size=kernel_size, stride=stride,
+                              padding=kernel_size // 2)
+        self.pos_encoding = PositionalEncoding2D(d_model=d_model, mel_bins=mel_bins)
+        self.norm = nn.LayerNorm(d_model)
+        self.activation = nn.GELU()
+
+    def _w(self):
+        def build():
+            w = self.conv.weight  # (D, C, k) -> (D, k*C), frame-major like the im2col rows
+            return w.permute(0, 2, 1).reshape(w.shape[0], -1).contiguous()
+        return cached(self, "w", (self.conv.weight,), build)
+
+    def output_length(self, frames: int) -> int:
+        k, s, p = self.conv.kernel_size[0], self.conv.stride[0], self.conv.padding[0]
+        return (frames + 2 * p - k) // s + 1
+
+    def forward(self, mel_spectrogram: torch.Tensor) -> torch.Tensor:
+        B, F, C = mel_spectrogram.shape
+        k, s, p = self.conv.kernel_size[0], self.conv.stride[0], self.conv.padding[0]
+        D = self.conv.out_channels
+        L = self.output_length(F)
+        frames = max(F + 2 * p, (L - 1) * s + k)
+        buf = ops.pad_frames(mel_spectrogram, frames, p)
+        x = torch.empty((B, L, D), device=buf.device, dtype=torch.float32)
+        ops.gemm_batched(buf, s * C, frames * C, L, B, k * C, self._w(), self.conv.bias, x, D, L * D,
+                         epilogue=_lib.EPI_GELU_PE, aux=self.pos_encoding.table(L), ld_aux=D, stride_aux=0)
+        return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
+
+
+class CTCOutputHead(nn.Module):
+    """LayerNorm -> Dropout -> Linear(d_model, vocab) (reference model.py:205-239)."""
+
+    def __init__(self, d_model: int = 192, vocab_size: int = 50000, dropout: float = 0.1):
+        super().__init__()
+        self.proj = nn.Sequential(nn.LayerNorm(d_model), nn.Dropout(dropout), nn.Linear(d_model, vocab_size))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, L, D = x.shape
+        ln, lin = self.proj[0], self.proj[2]
+        h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
+        return ops.gemm(h.view(B * L, D), lin.weight, lin.bias).view(B, L, lin.out_features)
+
+
+class VELOCITYASR(nn.Module):
+    """VELOCITY-ASR v2 (reference model.py:242-471)."""
+
+    def __init__(self, config: Optional[VelocityASRConfig] = None):
+        super().__init__()
+        if config is None:
+            config = VelocityASRConfig()
+        self.config = config
+        self.temporal_binding = TemporalBindingLayer(mel_bins=config.mel_bins, d_model=config.d_model)
+        self.local_ssm = LocalSSMProcessor(d_model=config.d_model, num_layers=config.ssm_layers,
+                                           state_dim=config.ssm_state_dim, expand_ratio=config.ssm_expand_ratio,
+                                           kernel_size=config.ssm_kernel_size, dropout=config.dropout,
+                                           use_checkpoint=config.gradient_checkpointing, scan_mode=config.scan_mode)
+        self.global_context = HierarchicalGlobalContext(d_model=config.d_model, num_heads=config.attention_heads,
+                                                        attention_dim=config.attention_dim,
+                                                        global_ssm_layers=config.global_ssm_layers,
+                                                        global_ssm_state_dim=config.global_ssm_state_dim,
+                                                        dropout=config.dropout)
+        self.ctc_head = CTCOutputHead(d_model=config.d_model, vocab_size=config.vocab_size, dropout=config.dropout)
+        self._init_weights()
+        # config.use_compile: the reference wraps submodules in torch.compile
+        # (model.py:320-331); here the whole forward is already native HIP and can be
+        # captured in a HIP graph (velocity_asr.pipeline.GraphedTranscriber) instead.
+
+    def _init_weights(self):
+        """Same initialisers, same order as the reference (model.py:305-318)."""
+        for module in self.modules():
+            if isinstance(module, nn.Linear):
+                nn.init.xavier_uniform_(module.weight)
+                if module.bias is not None:
+                    nn.init.zeros_(module.bias)
+            elif isinstance(module, nn.Conv1d):
+                nn.init.kaiming_normal_(module.weight, mode="fan_out", nonlinearity="relu")
+                if module.bias is not None:
+                    nn.init.zeros_(module.bias)
+            elif isinstance(module, nn.LayerNorm):
+                nn.init.ones_(module.weight)
+                nn.init.zeros_(module.bias)
+
+    def forward(self, mel_spectrogram: torch.Tensor, return_features: bool = False):
+        """(B, frames, mel_bins) -> CTC logits (B, (frames + 1) // 2, vocab_size)."""
+        if mel_spectrogram.device.type != "cuda":
+            _lib.require_device()
+            raise RuntimeError("velocity_asr (MI355X build): move the model and input to the HIP device "
+                               "(model.to('cuda'), mel.to('cuda')); there is no CPU execution path")
+        mel = mel_spectrogram.to(torch.float32)
+        with torch.no_grad():
+            x = self.temporal_binding(mel)
+            local_features = self.local_ssm(x)
+            fused_features = self.global_context(local_features)
+            logits = self.ctc_head(fused_features)
+        if return_features:
+            return logits, {"temporal_binding": x, "local_features": local_features,
+                            "fused_features": fused_features}
+        return logits
+
+    def get_output_length(self, input_length: int) -> int:
+        return (input_length + 1) // 2
+
+    @classmethod
+    def from_pretrained(cls, model_name_or_path: str, quantized: bool = False, **kwargs) -> "VELOCITYASR":
+        """Load a checkpoint written by save_pretrained or Trainer (reference model.py:385-433)."""
+        if not os.path.exists(model_name_or_path):
+            raise NotImplementedError("Model hub download not yet implemented. "
+                                      "Please provide a local path to the checkpoint.")
+        checkpoint = torch.load(model_name_or_path, map_location="cpu", weights_only=True)
+        if "config" in checkpoint:
+            config = VelocityASRConfig.from_dict(checkpoint["config"])
+        else:
+            config = VelocityASRConfig()
+        model = cls(config)
+        if "model_state_dict" in checkpoint:
+            model.load_state_dict(checkpoint["model_state_dict"])
+        else:
+            model.load_state_dict(checkpoint)
+        return model
+
+    def save_pretrained(self, save_path: str):
+        """Same on-disk format as the reference (model.py:435-467)."""
+        d = os.path.dirname(save_path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        c = self.config
+        checkpoint = {
+            "config": {
+                "mel_bins": c.mel_bins, "d_model": c.d_model, "ssm_layers": c.ssm_layers,
+                "ssm_state_dim": c.ssm_state_dim, "ssm_expand_ratio": c.ssm_expand_ratio,
+                "ssm_kernel_size": c.ssm_kernel_size, "global_ssm_layers": c.global_ssm_layers,
+                "global_ssm_state_dim": c.global_ssm_state_dim, "attention_heads": c.attention_heads,
+                "attention_dim": c.attention_dim, "vocab_size": c.vocab_size, "dropout": c.dropout,
+                "gradient_checkpointing": c.gradient_checkpointing, "scan_mode": c.scan_mode,
+                "use_compile": c.use_compile,
+            },
+            "model_state_dict": {k: v.detach().cpu() for k, v in self.state_dict().items()},
+        }
+        torch.save(checkpoint, save_path)
+
+    def count_parameters(self) -> int:
+        return sum(p.numel() for p in self.parameters() if p.requires_grad)

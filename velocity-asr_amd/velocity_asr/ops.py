@@ -1,0 +1,239 @@
+"""Thin tensor-level wrappers over the HIP kernels of libvasr_hip.so.
+
+Each wrapper validates device / dtype / layout on the host (raising ValueError or
+RuntimeError like torch would), allocates its output with the torch caching allocator
+and enqueues the kernel on the current HIP stream.  Nothing here computes on the CPU.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib as L
+from ._lib import GemmArgs, check, ptr, stream_of
+
+LOG2E = 1.4426950408889634
+
+
+def _cuda_f32(name: str, t: torch.Tensor) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{name}: tensor is on {t.device}; velocity_asr (MI355X build) runs on HIP devices only")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+
+
+def _rows(name: str, t: torch.Tensor) -> Tuple[int, int, int]:
+    """(rows, cols, row_stride) of a 2-D row-major view with unit column stride."""
+    if t.dim() != 2:
+        raise ValueError(f"{name}: expected a 2-D view, got shape {tuple(t.shape)}")
+    if t.stride(1) != 1 and t.shape[1] > 1:
+        raise ValueError(f"{name}: columns must be contiguous")
+    return t.shape[0], t.shape[1], t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, epilogue: int = L.EPI_NONE,
+         out: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
+         aux2: Optional[torch.Tensor] = None, n_out: int = 0, n_cols_out: Optional[int] = None) -> torch.Tensor:
+    """out = epilogue(a @ w.T + bias) for a (M, K) row view and w (N, K)."""
+    _cuda_f32("gemm.a", a)
+    _cuda_f32("gemm.w", w)
+    M, K, lda = _rows("gemm.a", a)
+    N, Kw, ldw = _rows("gemm.w", w)
+    if Kw != K:
+        raise ValueError(f"gemm: a has K={K} but w has K={Kw}")
+    cols = n_cols_out if n_cols_out is not None else (n_out if epilogue in (L.EPI_PAIR_POWER, L.EPI_PAIR_FUSION) else N)
+    if out is None:
+        out = torch.empty((M, cols), device=a.device, dtype=torch.float32)
+    _, _, ldc = _rows("gemm.out", out)
+    args = GemmArgs()
+    args.A, args.lda, args.stride_a = a.data_ptr(), lda, 0
+    args.W, args.ldw = w.data_ptr(), ldw
+    args.bias = ptr(bias)
+    args.C, args.ldc, args.stride_c = out.data_ptr(), ldc, 0
+    args.batch, args.M, args.N, args.K = 1, M, N, K
+    args.epilogue = epilogue
+    if aux is not None:
+        _, _, ld_aux = _rows("gemm.aux", aux)
+        args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, 0
+    args.aux2 = ptr(aux2)
+    args.n_out = n_out
+    check(L.lib().vasr_linear_f32(args, stream_of(a)), "vasr_linear_f32")
+    return out
+
+
+def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch: int, K: int, w: torch.Tensor,
+                 bias: Optional[torch.Tensor], out: torch.Tensor, ldc: int, stride_c: int, *,
+                 epilogue: int = L.EPI_NONE, aux: Optional[torch.Tensor] = None, ld_aux: int = 0,
+                 stride_aux: int = 0, n_out: int = 0) -> torch.Tensor:
+    """Strided batched form: A[b] rows at a_base + b*stride_a + m*lda (overlapping rows allowed)."""
+    _cuda_f32("gemm_batched.a", a_base)
+    _cuda_f32("gemm_batched.w", w)
+    need = (batch - 1) * stride_a + (rows - 1) * lda + K
+    avail = a_base.untyped_storage().nbytes() // 4 - a_base.storage_offset()
+    if rows > 0 and batch > 0 and need > avail:
+        raise ValueError(f"gemm_batched: A view needs {need} elements, {avail} available")
+    N, Kw, ldw = _rows("gemm_batched.w", w)
+    if Kw != K:
+        raise ValueError("gemm_batched: K mismatch")
+    args = GemmArgs()
+    args.A, args.lda, args.stride_a = a_base.data_ptr(), lda, stride_a
+    args.W, args.ldw = w.data_ptr(), ldw
+    args.bias = ptr(bias)
+    args.C, args.ldc, args.stride_c = out.data_ptr(), ldc, stride_c
+    args.batch, args.M, args.N, args.K = batch, rows, N, K
+    args.epilogue = epilogue
+    if aux is not None:
+        args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, stride_aux
+    args.n_out = n_out
+    check(L.lib().vasr_linear_f32(args, stream_of(a_base)), "vasr_linear_f32")
+    return out
+
+
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _cuda_f32("layer_norm.x", x)
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C)
+    rows, _, ldx = _rows("layer_norm.x", x2)
+    y = torch.empty((rows, C), device=x.device, dtype=torch.float32) if out is None else out.reshape(-1, C)
+    _, _, ldy = _rows("layer_norm.out", y)
+    check(L.lib().vasr_layer_norm_f32(x2.data_ptr(), ldx, w.data_ptr(), b.data_ptr(), y.data_ptr(), ldy, rows, C,
+                                      float(eps), stream_of(x)), "vasr_layer_norm_f32")
+    return y.view(*x.shape[:-1], C) if out is None else out
+
+
+def add_table(x: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """x (B, L, C) + table (L, C) broadcast over the batch."""
+    _cuda_f32("add_table.x", x)
+    _cuda_f32("add_table.table", table)
+    x = x.contiguous()
+    B, Lq, C = x.shape
+    if tuple(table.shape) != (Lq, C):
+        raise ValueError("add_table: table must be (L, C)")
+    out = torch.empty_like(x)
+    check(L.lib().vasr_add_table_f32(x.data_ptr(), table.contiguous().data_ptr(), out.data_ptr(), B, Lq, C,
+                                     stream_of(x)), "vasr_add_table_f32")
+    return out
+
+
+def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) -> torch.Tensor:
+    """(B, L, C) -> causal depthwise conv of LayerNorm(x)."""
+    _cuda_f32("ln_dwconv.x", x)
+    x = x.contiguous()
+    B, Lq, C = x.shape
+    Kc = conv_w.shape[-1]
+    y = torch.empty_like(x)
+    check(L.lib().vasr_ln_dwconv_f32(x.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+                                     conv_w.contiguous().data_ptr(), conv_b.data_ptr(), y.data_ptr(), B, Lq, C, Kc,
+                                     float(eps), stream_of(x)), "vasr_ln_dwconv_f32")
+    return y
+
+
+def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Tensor, D: torch.Tensor, B: int,
+             Lq: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Gated selective scan.  xz (B*L, 2Di) [x|z], dt (B*L, Di), bc (B*L, 2N) [B|C] (row views)."""
+    for n, t in (("xz", xz), ("dt", dt), ("bc", bc), ("A2", A2), ("D", D)):
+        _cuda_f32(f"ssm_scan.{n}", t)
+    M, two_di, ld_xz = _rows("ssm_scan.xz", xz)
+    _, Di, ld_dt = _rows("ssm_scan.dt", dt)
+    _, two_n, ld_bc = _rows("ssm_scan.bc", bc)
+    if M != B * Lq or two_di != 2 * Di or two_n != 2 * A2.numel() or D.numel() != Di:
+        raise ValueError("ssm_scan: inconsistent shapes")
+    if out is None:
+        out = torch.empty((M, Di), device=xz.device, dtype=torch.float32)
+    _, _, ld_out = _rows("ssm_scan.out", out)
+    check(L.lib().vasr_ssm_scan_f32(xz.data_ptr(), ld_xz, dt.data_ptr(), ld_dt, bc.data_ptr(), ld_bc, A2.data_ptr(),
+                                    D.data_ptr(), out.data_ptr(), ld_out, B, Lq, Di, A2.numel(), int(mode),
+                                    stream_of(xz)), "vasr_ssm_scan_f32")
+    return out
+
+
+def reflect_pad(audio: torch.Tensor, pad: int, ld_out: int) -> torch.Tensor:
+    _cuda_f32("reflect_pad.audio", audio)
+    audio = audio.contiguous()
+    B, S = audio.shape
+    xp = torch.empty((B, ld_out), device=audio.device, dtype=torch.float32)
+    check(L.lib().vasr_reflect_pad_f32(audio.data_ptr(), S, xp.data_ptr(), ld_out, B, S, pad, stream_of(audio)),
+          "vasr_reflect_pad_f32")
+    return xp
+
+
+def mel_log_norm(power: torch.Tensor, ld_power: int, stride_power: int, fb_csr, B: int, F: int, n_mels: int,
+                 normalize: bool) -> torch.Tensor:
+    rowptr, col, val = fb_csr
+    out = torch.empty((B, F, n_mels), device=power.device, dtype=torch.float32)
+    ws = torch.empty((B, F, n_mels), device=power.device, dtype=torch.float32)
+    check(L.lib().vasr_mel_log_norm_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(), col.data_ptr(),
+                                        val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F, n_mels, int(normalize),
+                                        ws.data_ptr(), stream_of(power)), "vasr_mel_log_norm_f32")
+    return out
+
+
+def pad_frames(x: torch.Tensor, out_frames: int, off: int) -> torch.Tensor:
+    _cuda_f32("pad_frames.x", x)
+    x = x.contiguous()
+    B, F, C = x.shape
+    out = torch.empty((B, out_frames, C), device=x.device, dtype=torch.float32)
+    check(L.lib().vasr_pad_frames_f32(x.data_ptr(), out.data_ptr(), out_frames, off, B, F, C, stream_of(x)),
+          "vasr_pad_frames_f32")
+    return out
+
+
+def adaptive_pool(x: torch.Tensor, K: int) -> torch.Tensor:
+    _cuda_f32("adaptive_pool.x", x)
+    x = x.contiguous()
+    B, Lq, C = x.shape
+    out = torch.empty((B, K, C), device=x.device, dtype=torch.float32)
+    check(L.lib().vasr_adaptive_pool_f32(x.data_ptr(), out.data_ptr(), B, Lq, C, K, stream_of(x)),
+          "vasr_adaptive_pool_f32")
+    return out
+
+
+def pooled_attention(q: torch.Tensor, kv: torch.Tensor, B: int, Lq: int, Kp: int, heads: int) -> torch.Tensor:
+    _cuda_f32("pooled_attention.q", q)
+    _cuda_f32("pooled_attention.kv", kv)
+    M, A, ld_q = _rows("pooled_attention.q", q)
+    kv = kv.contiguous()
+    if kv.shape != (B * Kp, 2 * A) or M != B * Lq or A % heads:
+        raise ValueError("pooled_attention: inconsistent shapes")
+    out = torch.empty((M, A), device=q.device, dtype=torch.float32)
+    check(L.lib().vasr_pooled_attention_f32(q.data_ptr(), ld_q, kv.data_ptr(), out.data_ptr(), B, Lq, Kp, heads,
+                                            A // heads, stream_of(q)), "vasr_pooled_attention_f32")
+    return out
+
+
+def argmax(logits: torch.Tensor) -> torch.Tensor:
+    """int32 argmax over the last dim (ties -> first index)."""
+    _cuda_f32("argmax.logits", logits)
+    V = logits.shape[-1]
+    x2 = logits.reshape(-1, V)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    rows = x2.shape[0]
+    ld = x2.stride(0) if rows > 1 else V
+    out = torch.empty(rows, device=logits.device, dtype=torch.int32)
+    check(L.lib().vasr_argmax_f32(x2.data_ptr(), ld, rows, V, out.data_ptr(), stream_of(logits)), "vasr_argmax_f32")
+    return out.view(logits.shape[:-1])
+
+
+def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, timestamps: bool = False):
+    """Device-side greedy CTC collapse of (B, L) int32 predictions."""
+    if pred.device.type != "cuda" or pred.dtype != torch.int32:
+        raise TypeError("ctc_collapse: expected a cuda int32 tensor")
+    pred = pred.contiguous()
+    B, Lq = pred.shape
+    toks = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
+    lens = torch.empty((B,), device=pred.device, dtype=torch.int32)
+    st = en = None
+    if timestamps:
+        st = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
+        en = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
+    check(L.lib().vasr_ctc_collapse(pred.data_ptr(), B, Lq, int(blank), int(collapse), toks.data_ptr(),
+                                    lens.data_ptr(), ptr(st), ptr(en), stream_of(pred)), "vasr_ctc_collapse")
+    return toks, lens, st, en

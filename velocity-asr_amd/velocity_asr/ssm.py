@@ -1,0 +1,166 @@
+"""Selective SSM blocks (drop-in for reference velocity_asr/ssm.py) on MI355X kernels.
+
+Same module tree, parameter names and shapes as the reference, so state_dicts load
+unchanged.  Forward passes run the HIP kernels of libvasr_hip.so:
+
+  SSMBlock:  LN1 + causal depthwise conv (one kernel)
+             -> in_proj GEMM (fp32 MFMA)
+             -> [x_proj; dt_proj] as ONE GEMM with bias + softplus fused on the dt columns
+             -> gated selective scan (tree or recurrence) with D skip and y*silu(z) fused
+             -> out_proj GEMM with the residual add fused
+             -> LN2 -> FFN1 GEMM + GELU -> FFN2 GEMM + bias + residual
+Inference only: dropout is the identity (as in eval()), no autograd.
+"""
+
+from __future__ import annotations
+
+import math
+import warnings
+from typing import Literal
+
+import torch
+import torch.nn as nn
+
+from . import _lib, ops
+from ._prep import cached
+
+ScanMode = Literal["sequential", "parallel", "mamba"]
+
+# The reference imports mamba_ssm's selective_scan_fn for scan_mode="mamba"
+# (ssm.py:20-26).  Here that operator contract is served by the HIP recurrence kernel
+# (vasr_ssm_scan_f32 mode 1, the semantics selective_scan_fn computes), so the mode is
+# always available.
+MAMBA_AVAILABLE = True
+
+_SCAN_MODE_ID = {"parallel": 0, "sequential": 1, "mamba": 1}
+_warned_training = False
+
+
+def _check_eval(module: nn.Module) -> None:
+    global _warned_training
+    if module.training and not _warned_training:
+        _warned_training = True
+        warnings.warn("velocity_asr (MI355X build) is inference-only: dropout is treated as identity; "
+                      "call model.eval() to silence this warning", stacklevel=3)
+
+
+class SelectiveSSM(nn.Module):
+    """Selective state space model (reference ssm.py:32-337)."""
+
+    def __init__(self, d_model: int = 192, state_dim: int = 64, expand_ratio: int = 2,
+                 scan_mode: ScanMode = "parallel"):
+        super().__init__()
+        self.d_model = d_model
+        self.state_dim = state_dim
+        self.d_inner = d_model * expand_ratio
+        self.scan_mode = scan_mode
+        if scan_mode not in _SCAN_MODE_ID:
+            raise ValueError(f"Unknown scan_mode: {scan_mode}")
+        self.in_proj = nn.Linear(d_model, self.d_inner * 2, bias=False)
+        self.x_proj = nn.Linear(self.d_inner, state_dim * 2, bias=False)
+        self.dt_proj = nn.Linear(self.d_inner, self.d_inner, bias=True)
+        A = torch.arange(1, state_dim + 1, dtype=torch.float32)
+        self.A_log = nn.Parameter(torch.log(A))
+        self.D = nn.Parameter(torch.ones(self.d_inner))
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=False)
+
+    def _prepared(self):
+        def build():
+            dev = self.x_proj.weight.device
+            w = torch.cat([self.x_proj.weight, self.dt_proj.weight], 0).contiguous()
+            b = torch.cat([torch.zeros(2 * self.state_dim, device=dev), self.dt_proj.bias]).contiguous()
+            # A = -exp(A_log) exactly as the reference evaluates it (float32, ssm.py:116), then
+            # pre-scaled by log2(e) so the kernel's dA is one v_exp_f32.
+            A = -torch.exp(self.A_log.detach().float().cpu())
+            A2 = (A * torch.tensor(ops.LOG2E, dtype=torch.float32)).to(dev)
+            return dict(w_xdt=w, b_xdt=b, A2=A2)
+        return cached(self, "ssm", (self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, self.A_log),
+                      build)
+
+    def gated_scan(self, u: torch.Tensor, B: int, L: int) -> torch.Tensor:
+        """u (B*L, d_model) -> y * silu(z) of shape (B*L, d_inner), before out_proj."""
+        p = self._prepared()
+        Di, N = self.d_inner, self.state_dim
+        xz = ops.gemm(u, self.in_proj.weight)                                   # (M, 2Di) [x | z]
+        xdt = ops.gemm(xz[:, :Di], p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM,
+                       n_out=2 * N)                                              # (M, 2N + Di) [B | C | dt]
+        return ops.ssm_scan(xz, xdt[:, 2 * N:], xdt[:, :2 * N], p["A2"], self.D, B, L,
+                            _SCAN_MODE_ID[self.scan_mode])
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _check_eval(self)
+        B, L, _ = x.shape
+        g = self.gated_scan(x.reshape(B * L, -1), B, L)
+        return ops.gemm(g, self.out_proj.weight).view(B, L, self.d_model)
+
+
+class SSMBlock(nn.Module):
+    """Pre-norm conv + SSM + FFN block (reference ssm.py:340-441)."""
+
+    def __init__(self, d_model: int = 192, state_dim: int = 64, expand_ratio: int = 2, kernel_size: int = 4,
+                 dropout: float = 0.1, use_checkpoint: bool = False, scan_mode: ScanMode = "parallel"):
+        super().__init__()
+        self.use_checkpoint = use_checkpoint
+        self.norm1 = nn.LayerNorm(d_model)
+        self.norm2 = nn.LayerNorm(d_model)
+        self.conv = nn.Conv1d(d_model, d_model, kernel_size=kernel_size, padding=kernel_size - 1, groups=d_model)
+        self.ssm = SelectiveSSM(d_model=d_model, state_dim=state_dim, expand_ratio=expand_ratio, scan_mode=scan_mode)
+        self.ffn = nn.Sequential(
+            nn.Linear(d_model, d_model * expand_ratio),
+            nn.GELU(),
+            nn.Dropout(dropout),
+            nn.Linear(d_model * expand_ratio, d_model),
+            nn.Dropout(dropout),
+        )
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _check_eval(self)
+        B, L, D = x.shape
+        x = x.contiguous()
+        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, self.conv.weight.view(D, -1), self.conv.bias,
+                          self.norm1.eps)
+        g = self.ssm.gated_scan(u.view(B * L, D), B, L)
+        x2 = x.view(B * L, D)
+        x1 = ops.gemm(g, self.ssm.out_proj.weight, epilogue=_lib.EPI_RESIDUAL, aux=x2)
+        h = ops.layer_norm(x1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        f = ops.gemm(h, self.ffn[0].weight, self.ffn[0].bias, epilogue=_lib.EPI_GELU)
+        out = ops.gemm(f, self.ffn[3].weight, self.ffn[3].bias, epilogue=_lib.EPI_RESIDUAL, aux=x1)
+        return out.view(B, L, D)
+
+
+class LocalSSMProcessor(nn.Module):
+    """Stack of SSM blocks + final LayerNorm (reference ssm.py:444-505)."""
+
+    def __init__(self, d_model: int = 192, num_layers: int = 8, state_dim: int = 64, expand_ratio: int = 2,
+                 kernel_size: int = 4, dropout: float = 0.1, use_checkpoint: bool = False,
+                 scan_mode: ScanMode = "parallel"):
+        super().__init__()
+        self.layers = nn.ModuleList([
+            SSMBlock(d_model=d_model, state_dim=state_dim, expand_ratio=expand_ratio, kernel_size=kernel_size,
+                     dropout=dropout, use_checkpoint=use_checkpoint, scan_mode=scan_mode)
+            for _ in range(num_layers)
+        ])
+        self.norm = nn.LayerNorm(d_model)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        for layer in self.layers:
+            x = layer(x)
+        return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
+
+
+class GlobalSSM(nn.Module):
+    """SSM over pooled tokens; always the default 'parallel' scan (reference ssm.py:508-556)."""
+
+    def __init__(self, d_model: int = 192, num_layers: int = 2, state_dim: int = 32, dropout: float = 0.1):
+        super().__init__()
+        self.layers = nn.ModuleList([
+            SSMBlock(d_model=d_model, state_dim=state_dim, expand_ratio=2, kernel_size=4, dropout=dropout)
+            for _ in range(num_layers)
+        ])
+        self.norm = nn.LayerNorm(d_model)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        for layer in self.layers:
+            x = layer(x)
+        return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
