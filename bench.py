@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: VELOCITY-ASR inference, audio -> CTC tokens, on MI355X.
+
+Workload (BASELINE.json configs[1]): the 6.17 M-parameter fp32 model, batch of 32 synthetic
+10 s clips at 16 kHz per GPU.  One step = reflect pad + DFT-GEMM log-mel + full forward
+(temporal binding, 8 SSM blocks, hierarchical global context, CTC head) + argmax + greedy
+collapse, on audio already resident in HBM, replayed as one HIP graph.  Multi-GPU: one
+process per GPU (torchrun), each rank transcribes its own 32 clips (utterance sharding, no
+data-path collective; weak scaling); a barrier + synchronize brackets the K timed steps
+and the max time over ranks is used.
+
+Prints ONE JSON line (rank 0):
+  value         = RTFx = audio seconds transcribed by all ranks / wall seconds
+  roofline      = the dominant kernel family measured live with HIP events (eager replay of
+                  the same steps on the launch stream) against the MI355X peak
+  cpu_baseline  = the numpy restatement of the reference path (oracle/) on this host, a
+                  bounded sample of the same workload (rank 0, N=1 only)
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, "velocity-asr_amd"), REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+SR = 16000
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TFS = 157.3    # dense f32-input MFMA = f32 vector peak
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(device):
+    import velocity_asr as va
+    from velocity_asr import synthetic as S
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    return m.to(device).eval()
+
+
+def kernel_roofline(model, audio, steps):
+    """Per-launch times of the scan and GEMM families over `steps` eager steps (HIP events)."""
+    from velocity_asr import ops
+    from velocity_asr.pipeline import audio_to_token_ids
+    with ops.kernel_timer("ssm_scan", "gemm") as kt:
+        for _ in range(steps):
+            audio_to_token_ids(model, audio)
+    rec = kt.summary()
+    out = {}
+    # selective scan of the 8 local blocks (N=64): bytes = B*L*(4*Di + 2*N)*4 per launch
+    scans = [(dt, i) for dt, i in rec["ssm_scan"] if i["N"] == model.config.ssm_state_dim]
+    if scans:
+        i = scans[0][1]
+        bytes_per = i["B"] * i["L"] * (4 * i["Di"] + 2 * i["N"]) * 4
+        elems = i["B"] * i["L"] * i["Di"] * i["N"]
+        t = float(np.mean([d for d, _ in scans]))
+        out["scan"] = dict(t=t, bytes=bytes_per, elems=elems, launches=len(scans), per_step=len(scans) / steps,
+                           total=sum(d for d, _ in scans) / steps)
+    g = rec["gemm"]
+    flops = [2.0 * i["M"] * i["N"] * i["K"] * i["batch"] for _, i in g]
+    out["gemm"] = dict(t=float(np.mean([d for d, _ in g])), flops=float(np.mean(flops)), launches=len(g),
+                       per_step=len(g) / steps, total=sum(d for d, _ in g) / steps,
+                       tflops=sum(flops) / max(sum(d for d, _ in g), 1e-12) / 1e12)
+    return out
+
+
+def cpu_baseline(seconds_target=12.0):
+    """Oracle (numpy port of the reference path) on 10 s clips until ~seconds_target of work."""
+    from oracle import velocity_ref as R
+    from velocity_asr import synthetic as S
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    W = S.make_weights(None, seed=0)
+    cfg = dict(S.DEFAULT_CONFIG)
+    clips, t0 = 0, time.perf_counter()
+    while True:
+        a = S.make_audio(1, 10 * SR, seed=1234 + clips)
+        R.ctc_greedy_decode(R.forward(W, R.compute_mel_spectrogram(a), cfg))
+        clips += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_target or clips >= 32:
+            break
+    return dict(value=round(clips * 10.0 / el, 3), unit="audio-sec/sec (RTFx)", cores=int(threads), kind="port",
+                sample=f"{clips} x 10 s clips, batch 1, mel+forward+greedy, oracle/velocity_ref.py "
+                       f"(numpy, BLAS threads={threads}), {el:.1f} s wall")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--seconds", type=float, default=10.0, help="clip length")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-steps", type=int, default=3)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from velocity_asr import synthetic as S
+    from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids
+
+    model = build_model(dev)
+    S_len = int(args.seconds * SR)
+    B = args.batch
+    audio = torch.from_numpy(S.make_audio(B, S_len, seed=1234 + rank)).to(dev)  # resident in HBM
+
+    if args.eager:
+        def step():
+            return audio_to_token_ids(model, audio)
+    else:
+        tr = GraphedTranscriber(model, B, S_len, dev)
+        tr.audio.copy_(audio)
+        step = tr.step
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # token checksum over all ranks (tiny gather, outside the timed region)
+    toks, lens = audio_to_token_ids(model, audio)
+    valid = torch.arange(toks.shape[1], device=dev)[None, :] < lens[:, None]
+    csum = torch.tensor([float(lens.sum().item()), float(toks.long().masked_fill(~valid, 0).sum().item())],
+                        device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(csum)
+
+    rf = kernel_roofline(model, audio, args.roofline_steps)
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    audio_sec = world * B * args.seconds * args.steps
+    frames = world * B * (S_len // 160 + 1) * args.steps
+    ms_per_step = elapsed / args.steps * 1e3
+    sc, gm = rf.get("scan"), rf["gemm"]
+    # dominant kernel family by measured time per step
+    if sc and sc["total"] >= gm["total"]:
+        ach = sc["bytes"] / sc["t"] / 1e9
+        roof = dict(bound="hbm", kernel="vasr ssm_scan (tree, local blocks)", achieved=round(ach, 1),
+                    peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), traffic=None,
+                    avg_launch_us=round(sc["t"] * 1e6, 2))
+    else:
+        ach = gm["flops"] / gm["t"] / 1e12
+        roof = dict(bound="mfma", kernel="vasr gemm_f32 (all projection GEMMs, mean launch)", achieved=round(ach, 2),
+                    peak=F32_MFMA_PEAK_TFS, unit="TFLOP/s", frac=round(ach / F32_MFMA_PEAK_TFS, 4), traffic=None,
+                    avg_launch_us=round(gm["t"] * 1e6, 2))
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            roof["traffic"] = json.load(open(pmc)).get(roof["kernel"].split(" ")[1])
+        except Exception:
+            pass
+    line = {
+        "metric": METRIC,
+        "value": round(audio_sec / elapsed, 2),
+        "unit": "audio-sec/sec (RTFx)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: N(0, 0.1) 16 kHz clips; seeded random-init weights (velocity_asr.synthetic)",
+        "config": {"workload": f"{B} x {args.seconds:g} s clips per GPU, audio->mel->forward->CTC greedy tokens "
+                               f"(BASELINE configs[1]{', HIP graph' if not args.eager else ', eager'})",
+                   "global_batch": world * B, "clip_seconds": args.seconds, "parallelism": f"utterance-shard x{world}"},
+        "frames_per_sec": round(frames / elapsed, 1),
+        "roofline": roof,
+        "kernels": {
+            "scan": None if not sc else dict(avg_launch_us=round(sc["t"] * 1e6, 2), launches_per_step=sc["per_step"],
+                                             ms_per_step=round(sc["total"] * 1e3, 3),
+                                             hbm_gbs=round(sc["bytes"] / sc["t"] / 1e9, 1),
+                                             gelem_per_s=round(sc["elems"] / sc["t"] / 1e9, 1)),
+            "gemm": dict(avg_launch_us=round(gm["t"] * 1e6, 2), launches_per_step=gm["per_step"],
+                         ms_per_step=round(gm["total"] * 1e3, 3), tflops=round(gm["tflops"], 2)),
+        },
+        "token_checksum": [int(csum[0].item()), int(csum[1].item())],
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline()
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -242,7 +242,6 @@ VASR_API int vasr_linear_f32(const vasr_gemm_args* a, void* stream) {
                    (long long)a->lda);
     VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->A) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->W) & 15) == 0,
                    "vasr_linear_f32: A and W must be 16-byte aligned");
-    VASR_CHECK_ARG(a->lda >= a->K || a->M <= 1, "vasr_linear_f32: lda < K");
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     if (pair) {

@@ -17,6 +17,47 @@ from ._lib import GemmArgs, check, ptr, stream_of
 
 LOG2E = 1.4426950408889634
 
+# Optional per-launch timing (bench.py roofline): while `_timing` is a dict, every launch of
+# a timed op records a (start, end, info) triple of HIP events on the launch stream.
+_timing = None
+
+
+class kernel_timer:
+    """Context manager: record HIP events around every launch of the named ops."""
+
+    def __init__(self, *names):
+        self.names = set(names)
+        self.records = {n: [] for n in names}
+
+    def __enter__(self):
+        global _timing
+        _timing = self
+        return self
+
+    def __exit__(self, *exc):
+        global _timing
+        _timing = None
+        return False
+
+    def summary(self):
+        torch.cuda.synchronize()
+        return {n: [(s.elapsed_time(e) * 1e-3, info) for s, e, info in recs] for n, recs in self.records.items()}
+
+
+def _t0(name):
+    if _timing is not None and name in _timing.names:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+    return None
+
+
+def _t1(name, start, info):
+    if start is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        _timing.records[name].append((start, ev, info))
+
 
 def _cuda_f32(name: str, t: torch.Tensor) -> None:
     if not isinstance(t, torch.Tensor):
@@ -63,7 +104,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
         args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, 0
     args.aux2 = ptr(aux2)
     args.n_out = n_out
+    ev = _t0("gemm")
     check(L.lib().vasr_linear_f32(args, stream_of(a)), "vasr_linear_f32")
+    _t1("gemm", ev, dict(M=M, N=N, K=K, batch=1))
     return out
 
 
@@ -91,7 +134,9 @@ def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch
     if aux is not None:
         args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, stride_aux
     args.n_out = n_out
+    ev = _t0("gemm")
     check(L.lib().vasr_linear_f32(args, stream_of(a_base)), "vasr_linear_f32")
+    _t1("gemm", ev, dict(M=rows, N=N, K=K, batch=batch))
     return out
 
 
@@ -148,9 +193,11 @@ def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Ten
     if out is None:
         out = torch.empty((M, Di), device=xz.device, dtype=torch.float32)
     _, _, ld_out = _rows("ssm_scan.out", out)
+    ev = _t0("ssm_scan")
     check(L.lib().vasr_ssm_scan_f32(xz.data_ptr(), ld_xz, dt.data_ptr(), ld_dt, bc.data_ptr(), ld_bc, A2.data_ptr(),
                                     D.data_ptr(), out.data_ptr(), ld_out, B, Lq, Di, A2.numel(), int(mode),
                                     stream_of(xz)), "vasr_ssm_scan_f32")
+    _t1("ssm_scan", ev, dict(B=B, L=Lq, Di=Di, N=A2.numel(), mode=int(mode)))
     return out
 
 
