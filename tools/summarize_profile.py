@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (gpurun_out/prof_<tag>) into profiles/<tag>_*.
+
+Writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_summary.md         per-kernel table: calls, avg us, share, HBM bytes/launch
+  profiles/pmc_traffic.json         per-kernel-family HBM bytes per launch, used by bench.py
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from separate
+--pmc passes (KiB units); FETCH_SIZE is doubled on gfx950 (it tallies 128-B requests at
+64 B; calibrated here on layer_norm_kernel, whose 12.3 MB read shows as 6.04 MB), WRITE_SIZE
+is taken as is (it matches the scan's 24.6 MB output exactly).
+"""
+
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    n = name.replace("void ", "").replace("vasr::(anonymous namespace)::", "")
+    return n.split("(")[0]
+
+
+def family(name):
+    n = short(name)
+    if n.startswith("ssm_scan_kernel<64, 0"):
+        return "ssm_scan"
+    if n.startswith("gemm_f32_kernel"):
+        return "gemm_f32"
+    return n.split("<")[0]
+
+
+def pmc(path, counter):
+    agg = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return agg
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            agg[(short(r["Kernel_Name"]), r["Grid_Size"])].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main(tag):
+    src = os.path.join(REPO, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(REPO, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = pmc(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    per_kernel = {}
+    for key in set(fetch) | set(write):
+        f = fetch.get(key, [0.0])
+        w = write.get(key, [0.0])
+        per_kernel[key] = (2 * 1024 * sum(f) / len(f), 1024 * sum(w) / len(w))
+    lines = [f"# rocprofv3 summary, run {tag}", "",
+             "| kernel | calls | avg us | share % | HBM read MB/launch | HBM write MB/launch |",
+             "|---|---|---|---|---|---|"]
+    traffic = {}
+    for r in rows:
+        n = short(r["Name"])
+        cands = [v for (k, g), v in per_kernel.items() if k == n]
+        rd = max((c[0] for c in cands), default=None)
+        wr = max((c[1] for c in cands), default=None)
+        lines.append(f"| `{n[:70]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
+                     f"{float(r['Percentage']):.2f} | {'' if rd is None else f'{rd / 1e6:.1f}'} | "
+                     f"{'' if wr is None else f'{wr / 1e6:.1f}'} |")
+        fam = family(r["Name"])
+        if fam in ("ssm_scan",) and rd is not None:
+            traffic[fam] = int(rd + wr)
+    with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
+        json.dump(dict(run=tag, unit="bytes per launch (FETCH_SIZE*2 + WRITE_SIZE)", **traffic), f, indent=1)
+    print("\n".join(lines[:14]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
