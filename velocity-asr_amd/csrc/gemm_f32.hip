@@ -21,6 +21,10 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifndef VASR_GEMM_XCD
+#define VASR_GEMM_XCD 1   // XCD-aware tile order (diagnostic builds may turn it off)
+#endif
+
 constexpr int BK = 32;
 constexpr int SK = BK + 4;  // padded LDS row (floats)
 
@@ -39,10 +43,11 @@ struct GemmParams {
     int n_out;
 };
 
-template <int WM, int WN, int TM, int EPI>
+template <int WM, int WN, int TM, int TN, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
-    constexpr int BN = WN * 64;
+    constexpr int BN = WN * 32 * TN;
+    static_assert(TN == 2 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need TN=2");
     constexpr int A_LOADS = BM * (BK / 4) / 256;  // float4 per thread
     constexpr int W_LOADS = BN * (BK / 4) / 256;
     static_assert(A_LOADS >= 1 && W_LOADS >= 1, "tile too small");
@@ -59,9 +64,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     const int r = lane & 31;
     const int h = lane >> 5;
 
-    const int m0 = blockIdx.y * BM;
-    const int n0 = blockIdx.x * BN;
-    const int bz = blockIdx.z;
+    // Tile decode.  The grid is 1-D; blocks id, id + 8, id + 16, ... are dealt to the same XCD
+    // (round-robin dispatch), so each such group gets a contiguous, M-major run of tiles: all
+    // N tiles of an A row panel then run on one XCD and share its L2.
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles = tiles_n * tiles_m * (int)gridDim.y;
+    int w = blockIdx.x + (int)blockIdx.y * (int)gridDim.x;
+    if (VASR_GEMM_XCD) {
+        const int q8 = tiles / 8, r8 = tiles % 8, xg = w % 8;
+        w = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + w / 8;
+    }
+    const int per_batch = tiles_n * tiles_m;
+    const int bz = w / per_batch;
+    const int wr_ = w - bz * per_batch;
+    const int m0 = (wr_ / tiles_n) * BM;
+    const int n0 = (wr_ % tiles_n) * BN;
     const float* __restrict__ A = p.A + (int64_t)bz * p.stride_a;
     const float* __restrict__ W = p.W;
 
@@ -98,11 +116,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         }
     };
 
-    floatx16 acc[TM][2];
+    floatx16 acc[TM][TN];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < 2; ++tn)
+        for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[tm][tn][i] = 0.f;
 
@@ -112,20 +130,20 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     __syncthreads();
 
     const float* a_base = As + (wr * 32 * TM + r) * SK + h * 16;
-    const float* w_base = Ws + (wc * 64 + r) * SK + h * 16;
+    const float* w_base = Ws + (wc * 32 * TN + r) * SK + h * 16;
 
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + 1 < nk) load_tile((kt + 1) * BK);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
-            float4 fa[TM][2], fw[2][2];
+            float4 fa[TM][2], fw[TN][2];
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
                 fa[tm][0] = *reinterpret_cast<const float4*>(a_base + tm * 32 * SK + kh * 8);
                 fa[tm][1] = *reinterpret_cast<const float4*>(a_base + tm * 32 * SK + kh * 8 + 4);
             }
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
+            for (int tn = 0; tn < TN; ++tn) {
                 fw[tn][0] = *reinterpret_cast<const float4*>(w_base + tn * 32 * SK + kh * 8);
                 fw[tn][1] = *reinterpret_cast<const float4*>(w_base + tn * 32 * SK + kh * 8 + 4);
             }
@@ -135,7 +153,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
                 for (int tm = 0; tm < TM; ++tm) {
                     const float av = reinterpret_cast<const float*>(&fa[tm][s >> 2])[s & 3];
 #pragma unroll
-                    for (int tn = 0; tn < 2; ++tn) {
+                    for (int tn = 0; tn < TN; ++tn) {
                         const float bv = reinterpret_cast<const float*>(&fw[tn][s >> 2])[s & 3];
                         acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[tm][tn], 0, 0, 0);
                     }
@@ -154,7 +172,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     const float* __restrict__ auxb = p.aux ? p.aux + (int64_t)bz * p.stride_aux : nullptr;
 
     if constexpr (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) {
-        const int col = (n0 + wc * 64) / 2 + r;  // output column of this lane
+        const int col = (n0 + wc * 32 * TN) / 2 + r;  // output column of this lane
         if (col >= p.n_out) return;
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
@@ -163,13 +181,13 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
                 const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
                 if (row >= p.M) continue;
                 const float v0 = acc[tm][0][i];
-                const float v1 = acc[tm][1][i];
+                const float v1 = acc[tm][TN - 1][i];
                 float out;
                 if constexpr (EPI == VASR_EPI_PAIR_POWER) {
                     out = v0 * v0 + v1 * v1;
                 } else {
                     // aux: local-side partial products in the same paired layout.
-                    const int pc = n0 + wc * 64 + r;  // paired column of half 0
+                    const int pc = n0 + wc * 32 * TN + r;  // paired column of half 0
                     const float* ar = auxb + (int64_t)row * p.ld_aux;
                     const float gate = sigmoidf_((ar[pc] + v0) + p.bias[pc]);
                     const float lt = ar[pc + 32] + p.aux2[col];
@@ -183,8 +201,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
-                const int col = n0 + wc * 64 + tn * 32 + r;
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = n0 + wc * 32 * TN + tn * 32 + r;
                 if (col >= p.N) continue;
                 const float bv = p.bias ? p.bias[col] : 0.0f;
 #pragma unroll
@@ -209,23 +227,65 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     }
 }
 
-template <int WM, int WN, int TM>
+template <int WM, int WN, int TM, int TN>
 int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     constexpr int BM = WM * 32 * TM;
-    constexpr int BN = WN * 64;
-    dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, batch);
+    constexpr int BN = WN * 32 * TN;
+    const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+    dim3 grid(tiles, batch);
     dim3 block(256);
+#define VASR_L(E) hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, TN, E>), grid, block, 0, s, p)
     switch (epi) {
-        case VASR_EPI_NONE: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_NONE>), grid, block, 0, s, p); break;
-        case VASR_EPI_GELU: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_GELU>), grid, block, 0, s, p); break;
-        case VASR_EPI_SOFTPLUS_FROM: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_SOFTPLUS_FROM>), grid, block, 0, s, p); break;
-        case VASR_EPI_RESIDUAL: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_RESIDUAL>), grid, block, 0, s, p); break;
-        case VASR_EPI_GELU_PE: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_GELU_PE>), grid, block, 0, s, p); break;
-        case VASR_EPI_PAIR_POWER: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_PAIR_POWER>), grid, block, 0, s, p); break;
-        case VASR_EPI_PAIR_FUSION: hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, VASR_EPI_PAIR_FUSION>), grid, block, 0, s, p); break;
+        case VASR_EPI_NONE: VASR_L(VASR_EPI_NONE); break;
+        case VASR_EPI_GELU: VASR_L(VASR_EPI_GELU); break;
+        case VASR_EPI_SOFTPLUS_FROM: VASR_L(VASR_EPI_SOFTPLUS_FROM); break;
+        case VASR_EPI_RESIDUAL: VASR_L(VASR_EPI_RESIDUAL); break;
+        case VASR_EPI_GELU_PE: VASR_L(VASR_EPI_GELU_PE); break;
+        case VASR_EPI_PAIR_POWER:
+            if constexpr (TN == 2) { VASR_L(VASR_EPI_PAIR_POWER); break; }
+            set_error("vasr_linear_f32: paired epilogue needs a TN=2 tile"); return VASR_EINVAL;
+        case VASR_EPI_PAIR_FUSION:
+            if constexpr (TN == 2) { VASR_L(VASR_EPI_PAIR_FUSION); break; }
+            set_error("vasr_linear_f32: paired epilogue needs a TN=2 tile"); return VASR_EINVAL;
         default: set_error("vasr_linear_f32: unknown epilogue %d", epi); return VASR_EINVAL;
     }
+#undef VASR_L
     return launch_status("vasr_linear_f32");
+}
+
+// Tile configurations: {WM, WN, TM, TN, blocks per CU the kernel's VGPR/LDS use admits}.
+struct TileCfg {
+    int wm, wn, tm, tn, occ;
+    int bm() const { return wm * 32 * tm; }
+    int bn() const { return wn * 32 * tn; }
+};
+constexpr TileCfg kCfgs[] = {
+    {2, 2, 2, 2, 3},  // 128 x 128
+    {2, 2, 1, 2, 4},  //  64 x 128
+    {4, 1, 1, 2, 4},  // 128 x  64
+    {2, 2, 1, 1, 7},  //  64 x  64
+};
+constexpr int kCUs = 256;
+
+// Pick the tile that minimises (rounds of resident blocks) x (blocks sharing a CU) x tile area:
+// at M = 16032 the grids are only one or two rounds deep, so wave quantisation and CU
+// balance, not per-tile efficiency, decide the time (measured in tools/gemm_variants_run.py).
+int pick_cfg(int M, int N, int batch, bool pair) {
+    int best = -1;
+    double best_cost = 0;
+    for (int i = 0; i < 4; ++i) {
+        const TileCfg& c = kCfgs[i];
+        if (pair && c.tn != 2) continue;
+        const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
+        const long per_cu = (tiles + kCUs - 1) / kCUs;
+        const long rounds = (per_cu + c.occ - 1) / c.occ;
+        const double cost = (double)rounds * (double)(per_cu < c.occ ? per_cu : c.occ) * c.bm() * c.bn();
+        if (best < 0 || cost < best_cost * 0.999) {
+            best = i;
+            best_cost = cost;
+        }
+    }
+    return best;
 }
 
 }  // namespace
@@ -263,12 +323,10 @@ VASR_API int vasr_linear_f32(const vasr_gemm_args* a, void* stream) {
     p.aux2 = a->aux2; p.n_out = a->n_out;
     hipStream_t s = as_stream(stream);
 
-    // Tile choice: 128x128 for wide outputs; 128x64 when N is a multiple of 64 but not 128
-    // (N = 192 projections: three exact column tiles) or narrow.
-    const int64_t rows = (int64_t)a->M * a->batch;
-    if (a->N <= 64 || (a->N % 128 != 0 && a->N % 64 == 0 && a->N <= 256))
-        return launch_cfg<4, 1, 1>(p, a->batch, epi, s);
-    if (rows <= 4096)
-        return launch_cfg<2, 2, 1>(p, a->batch, epi, s);
-    return launch_cfg<2, 2, 2>(p, a->batch, epi, s);
+    switch (pick_cfg(a->M, a->N, a->batch, pair)) {
+        case 0: return launch_cfg<2, 2, 2, 2>(p, a->batch, epi, s);
+        case 1: return launch_cfg<2, 2, 1, 2>(p, a->batch, epi, s);
+        case 2: return launch_cfg<4, 1, 1, 2>(p, a->batch, epi, s);
+        default: return launch_cfg<2, 2, 1, 1>(p, a->batch, epi, s);
+    }
 }

@@ -16,29 +16,47 @@
 //
 // mode 1 is the true recurrence of scan_mode="sequential" (ssm.py:134-171).
 //
-// Work decomposition (MI355X): one workgroup = (utterance b, DPB consecutive channels d).
-// Within a wave, G = N/4 lanes share one channel and each lane owns 4 state indices n, so
-// the y[t] = sum_n h C contraction is 4 FMAs + log2(G) DPP adds (quad_perm / row mirrors,
-// no LDS).  Time is processed in 16-step chunks: the chunk's x, dt, z, B, C slices are
-// staged to LDS (double-buffered with a register prefetch of the next chunk), the four
-// in-chunk stack levels are compile-time registers (the push/merge pattern of step i is a
-// constant), and the upper levels (chunk-sized blocks) are merged once per chunk.  The
-// gated outputs of a chunk are written as coalesced row segments from an LDS tile.
+// Work decomposition (MI355X): one workgroup = (utterance b, DPB consecutive channels d),
+// 4 waves.  G = N/4 lanes share one channel and each lane owns 4 state indices n, held as
+// two float2 pairs so the state algebra issues as packed v_pk_mul/v_pk_add_f32 (two lanes'
+// worth of fp32 per instruction: the f32 vector peak).  Per time step each lane leaves its
+// partial y = sum_n h C in an LDS tile; the chunk's gated outputs are reduced and written
+// from LDS as coalesced row segments.  Time runs in 16-step chunks: x, dt, z, B, C slices
+// are staged to LDS (double-buffered, register prefetch of the next chunk); the four
+// in-chunk stack levels are compile-time registers (step i's push/merge pattern is a
+// constant, full chunks carry no per-step guards); chunk-sized blocks form the upper stack,
+// merged once per chunk.  Blocks are remapped so all channel blocks of one utterance share
+// an XCD (its 4 MiB L2 then serves the B/C slices and the 64-B row segments they share).
 #include "vasr_internal.h"
 
 namespace vasr {
 namespace {
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+#ifndef VASR_SCAN_ABLATE
+#define VASR_SCAN_ABLATE 0  // diagnostic builds only (tools/scan_ablate.sh): 1 no exp, 2 no partial
+#endif                      // write, 4 no B/C LDS reads, 8 no chunk staging after the first
+#ifndef VASR_SCAN_DPP
+#define VASR_SCAN_DPP 1     // reduce the per-step partial sums across the G lanes with DPP
+#endif
+#ifndef VASR_SCAN_WAVES
+#define VASR_SCAN_WAVES 3   // waves per SIMD the register allocator targets
+#endif
+
 constexpr int T = 16;    // time steps per chunk
-constexpr int NPL = 4;   // state indices per lane
+constexpr int NPL = 4;   // state indices per lane (2 packed pairs)
+constexpr int NP = NPL / 2;
+constexpr int NW = 4;    // waves per block
 
 constexpr int ctz_c(int v) { return v & 1 ? 0 : 1 + ctz_c(v >> 1); }
 constexpr int trailing_ones(int v) { return v & 1 ? 1 + trailing_ones(v >> 1) : 0; }
 // Level of the stack entry right below a new block at level j after step i (count i+1),
 // or -1 when the entry below is the upper (chunk-level) stack.
 constexpr int below_level(int i, int j) {
-    int rest = (i + 1) >> (j + 1);
-    return rest == 0 || j + 1 >= 4 ? -1 : (j + 1 + ctz_c(rest) < 4 ? j + 1 + ctz_c(rest) : -1);
+    return ((i + 1) >> (j + 1)) == 0 ? -1
+           : (j + 1 + ctz_c((i + 1) >> (j + 1)) < 4 ? j + 1 + ctz_c((i + 1) >> (j + 1)) : -1);
 }
 
 template <int CTRL>
@@ -58,272 +76,311 @@ __device__ __forceinline__ float group_sum(float v) {
 
 template <int MAXUP>
 struct TreeState {
-    float la[4][NPL], lb[4][NPL], ca[4][NPL], cb[4][NPL];  // in-chunk levels 0..3
-    float ula[MAXUP][NPL], ulb[MAXUP][NPL];                // chunk-level blocks
-    float pa[NPL], pb[NPL];                                // prefix after the upper stack
+    f2 la[4][NP], lb[4][NP], ca[4][NP], cb[4][NP];  // in-chunk levels 0..3
+    f2 ula[MAXUP][NP], ulb[MAXUP][NP];              // chunk-level blocks
+    f2 pa[NP], pb[NP];                              // prefix after the upper stack
 };
 
+struct Smem {
+    const float* xs;
+    const float* dts;
+    const float* bcs;
+    float* yp;  // partial sums [T][DPB][G]
+};
+
+// Per-step operands of one lane, read from the staged chunk one step ahead of use.
 struct StepIn {
     float x, dt;
-    float Bn[NPL], Cn[NPL];
+    float4 bv, cv;
 };
 
-// One push of the streaming tree scan at in-chunk step I.  Returns the partial
-// y contribution (sum over this lane's n of h[t] * C[t]).
-template <int I, int MAXUP>
-__device__ __forceinline__ float tree_step(TreeState<MAXUP>& s, const StepIn& in, const float (&A2)[NPL],
-                                           float (&chunk_a)[NPL], float (&chunk_b)[NPL]) {
-#pragma clang fp contract(off)
-    float part = 0.f;
-#pragma unroll
-    for (int n = 0; n < NPL; ++n) {
-        float hv;
-        if constexpr (I == 0) hv = s.pb[n];
-        else hv = s.cb[ctz_c(I)][n];
-        part = __builtin_fmaf(hv, in.Cn[n], part);
+template <int I, int N, int DPB>
+__device__ __forceinline__ StepIn load_step(const Smem& sm, int dl, int g) {
+    StepIn in;
+    in.x = sm.xs[I * DPB + dl];
+    in.dt = sm.dts[I * DPB + dl];
+    if constexpr (VASR_SCAN_ABLATE & 4) {
+        in.bv = make_float4(in.x, in.dt, in.x, in.dt);
+        in.cv = make_float4(in.dt, in.x, in.dt, in.x);
+    } else {
+        in.bv = *reinterpret_cast<const float4*>(sm.bcs + I * 2 * N + g * NPL);
+        in.cv = *reinterpret_cast<const float4*>(sm.bcs + I * 2 * N + N + g * NPL);
     }
-    constexpr int J = trailing_ones(I);
+    return in;
+}
+
+__device__ __forceinline__ f2 exp2v(f2 v) {
+    f2 r;
+    r.x = __builtin_amdgcn_exp2f(v.x);
+    r.y = __builtin_amdgcn_exp2f(v.y);
+    return r;
+}
+
+// One push of the streaming tree scan at in-chunk step I; stores this lane's partial y.
+template <int I, int MAXUP, int N, int DPB>
+__device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, const StepIn& in, const f2 (&A2)[NP],
+                                          int dl, int g, f2 (&chunk_a)[NP], f2 (&chunk_b)[NP]) {
+#pragma clang fp contract(off)
+    constexpr int G = N / NPL;
+    const float x = in.x;
+    const float dt = in.dt;
+    const f2 Bn[NP] = {{in.bv.x, in.bv.y}, {in.bv.z, in.bv.w}};
+    const f2 Cn[NP] = {{in.cv.x, in.cv.y}, {in.cv.z, in.cv.w}};
+    // y contribution of h[t] (the exclusive prefix = cb of the current top block)
+    f2 part;
 #pragma unroll
-    for (int n = 0; n < NPL; ++n) {
-        float cur_a = __builtin_amdgcn_exp2f(in.dt * A2[n]);
-        const float dB = in.dt * in.Bn[n];
-        float cur_b = in.x * dB;
+    for (int p = 0; p < NP; ++p) {
+        f2 hv;
+        if constexpr (I == 0) hv = s.pb[p];
+        else hv = s.cb[ctz_c(I)][p];
+        part = p == 0 ? hv * Cn[p] : part + hv * Cn[p];
+    }
+    if constexpr (VASR_SCAN_ABLATE & 2) {
+        if (part.x == 12345.f) sm.yp[(I * DPB + dl) * G + g] = part.y;
+    } else if constexpr (VASR_SCAN_DPP) {
+        const float y = group_sum<G>(part.x + part.y);
+        if (g == 0) sm.yp[I * DPB + dl] = y;
+    } else {
+        sm.yp[(I * DPB + dl) * G + g] = part.x + part.y;
+    }
+
+    constexpr int J = trailing_ones(I);
+    const f2 dt2 = {dt, dt};
+    const f2 x2 = {x, x};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        f2 cur_a = (VASR_SCAN_ABLATE & 1) ? dt2 * A2[p] : exp2v(dt2 * A2[p]);
+        const f2 dB = dt2 * Bn[p];
+        f2 cur_b = x2 * dB;
 #pragma unroll
         for (int k = 0; k < J; ++k) {  // up-sweep: (a_r, b_r) <- (a_r a_l, a_r b_l + b_r)
-            cur_b = cur_a * s.lb[k][n] + cur_b;
-            cur_a = cur_a * s.la[k][n];
+            cur_b = cur_a * s.lb[k][p] + cur_b;
+            cur_a = cur_a * s.la[k][p];
         }
         if constexpr (J < 4) {
-            s.la[J][n] = cur_a;
-            s.lb[J][n] = cur_b;
+            s.la[J][p] = cur_a;
+            s.lb[J][p] = cur_b;
             constexpr int BL = below_level(I, J);
-            float Pa, Pb;
+            f2 Pa, Pb;
             if constexpr (BL >= 0) {
-                Pa = s.ca[BL][n];
-                Pb = s.cb[BL][n];
+                Pa = s.ca[BL][p];
+                Pb = s.cb[BL][p];
             } else {
-                Pa = s.pa[n];
-                Pb = s.pb[n];
+                Pa = s.pa[p];
+                Pb = s.pb[p];
             }
-            const float c_a = Pa * cur_a;  // down-sweep: a_r <- a_p a_l ; b_r <- a_r b_l + b_p
-            s.ca[J][n] = c_a;
-            s.cb[J][n] = c_a * cur_b + Pb;
+            const f2 c_a = Pa * cur_a;  // down-sweep: a_r <- a_p a_l ; b_r <- a_r b_l + b_p
+            s.ca[J][p] = c_a;
+            s.cb[J][p] = c_a * cur_b + Pb;
         } else {
-            chunk_a[n] = cur_a;
-            chunk_b[n] = cur_b;
+            chunk_a[p] = cur_a;
+            chunk_b[p] = cur_b;
         }
     }
-    return part;
 }
 
 template <int MAXUP>
-__device__ __forceinline__ void merge_upper(TreeState<MAXUP>& s, float (&chunk_a)[NPL], float (&chunk_b)[NPL],
+__device__ __forceinline__ void merge_upper(TreeState<MAXUP>& s, const f2 (&chunk_a)[NP], const f2 (&chunk_b)[NP],
                                             int cc) {
 #pragma clang fp contract(off)
     const int j = __builtin_ctz(~cc);
+    const int cc1 = cc + 1;
 #pragma unroll
-    for (int n = 0; n < NPL; ++n) {
-        float cur_a = chunk_a[n], cur_b = chunk_b[n];
+    for (int p = 0; p < NP; ++p) {
+        f2 cur_a = chunk_a[p], cur_b = chunk_b[p];
 #pragma unroll
         for (int u = 0; u < MAXUP; ++u) {
             if (u < j) {
-                cur_b = cur_a * s.ulb[u][n] + cur_b;
-                cur_a = cur_a * s.ula[u][n];
+                cur_b = cur_a * s.ulb[u][p] + cur_b;
+                cur_a = cur_a * s.ula[u][p];
             }
         }
 #pragma unroll
         for (int u = 0; u < MAXUP; ++u) {
             if (u == j) {
-                s.ula[u][n] = cur_a;
-                s.ulb[u][n] = cur_b;
+                s.ula[u][p] = cur_a;
+                s.ulb[u][p] = cur_b;
             }
         }
-        // Prefix after the upper stack, rebuilt bottom-up with the stream form's (1, 0) start:
-        // identical float operations to carrying (ca, cb) per upper entry.
-        const int cc1 = cc + 1;
-        float pa = 1.0f, pb = 0.0f;
+        // Prefix after the upper stack, rebuilt bottom-up from the stream form's (1, 0) start:
+        // the same float operations as carrying (ca, cb) per upper entry.
+        f2 pa = {1.0f, 1.0f}, pb = {0.0f, 0.0f};
 #pragma unroll
         for (int u = MAXUP - 1; u >= 0; --u) {
             if ((cc1 >> u) & 1) {
-                pa = pa * s.ula[u][n];
-                pb = pa * s.ulb[u][n] + pb;
+                pa = pa * s.ula[u][p];
+                pb = pa * s.ulb[u][p] + pb;
             }
         }
-        s.pa[n] = pa;
-        s.pb[n] = pb;
+        s.pa[p] = pa;
+        s.pb[p] = pb;
     }
 }
 
-template <int I, int MAXUP, int G>
+template <int I, int MAXUP, int N, int DPB, bool FULL>
 struct TreeChunk {
-    __device__ __forceinline__ static void run(TreeState<MAXUP>& s, const float (&A2)[NPL], int nvalid,
-                                               const float* xs, const float* dts, const float* bcs, float* yt,
-                                               int dl, int g, int DPB, int N, float (&ca)[NPL], float (&cb)[NPL]) {
-        if (I < nvalid) {
-            StepIn in;
-            in.x = xs[I * DPB + dl];
-            in.dt = dts[I * DPB + dl];
-            const float4 bv = *reinterpret_cast<const float4*>(bcs + I * 2 * N + g * NPL);
-            const float4 cv = *reinterpret_cast<const float4*>(bcs + I * 2 * N + N + g * NPL);
-            in.Bn[0] = bv.x; in.Bn[1] = bv.y; in.Bn[2] = bv.z; in.Bn[3] = bv.w;
-            in.Cn[0] = cv.x; in.Cn[1] = cv.y; in.Cn[2] = cv.z; in.Cn[3] = cv.w;
-            float part = tree_step<I, MAXUP>(s, in, A2, ca, cb);
-            part = group_sum<G>(part);
-            if (g == 0) yt[I * DPB + dl] = part;
-            TreeChunk<I + 1, MAXUP, G>::run(s, A2, nvalid, xs, dts, bcs, yt, dl, g, DPB, N, ca, cb);
+    __device__ __forceinline__ static void run(TreeState<MAXUP>& s, const Smem& sm, const StepIn& cur,
+                                               const f2 (&A2)[NP], int dl, int g, int nvalid, f2 (&ca)[NP],
+                                               f2 (&cb)[NP]) {
+        if (FULL || I < nvalid) {
+            StepIn nxt;
+            if constexpr (I + 1 < T) nxt = load_step<I + 1, N, DPB>(sm, dl, g);  // one step ahead
+            tree_step<I, MAXUP, N, DPB>(s, sm, cur, A2, dl, g, ca, cb);
+            TreeChunk<I + 1, MAXUP, N, DPB, FULL>::run(s, sm, nxt, A2, dl, g, nvalid, ca, cb);
         }
     }
 };
-template <int MAXUP, int G>
-struct TreeChunk<T, MAXUP, G> {
-    __device__ __forceinline__ static void run(TreeState<MAXUP>&, const float (&)[NPL], int, const float*,
-                                               const float*, const float*, float*, int, int, int, int,
-                                               float (&)[NPL], float (&)[NPL]) {}
+template <int MAXUP, int N, int DPB, bool FULL>
+struct TreeChunk<T, MAXUP, N, DPB, FULL> {
+    __device__ __forceinline__ static void run(TreeState<MAXUP>&, const Smem&, const StepIn&, const f2 (&)[NP], int,
+                                               int, int, f2 (&)[NP], f2 (&)[NP]) {}
 };
 
 template <int N, int MODE, int MAXUP>
-__global__ __launch_bounds__(256) void ssm_scan_kernel(const float* __restrict__ xz, int64_t ld_xz,
+__global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const float* __restrict__ xz, int64_t ld_xz,
                                                        const float* __restrict__ dt, int64_t ld_dt,
                                                        const float* __restrict__ bc, int64_t ld_bc,
                                                        const float* __restrict__ A2g, const float* __restrict__ Dg,
-                                                       float* __restrict__ out, int64_t ld_out, int L, int Di) {
+                                                       float* __restrict__ out, int64_t ld_out, int B, int L,
+                                                       int Di) {
 #pragma clang fp contract(off)
     constexpr int G = N / NPL;       // lanes per channel
     constexpr int DPW = 64 / G;      // channels per wave
-    constexpr int NW = 4;            // waves per block
     constexpr int DPB = NW * DPW;    // channels per block
-    constexpr int MAXDPB = DPB;
-    // LDS: two staging buffers {x, dt, z: T x DPB; bc: T x 2N} + y tile T x DPB
-    constexpr int BUF = 3 * T * MAXDPB + T * 2 * N;
-    __shared__ __attribute__((aligned(16))) float smem[2 * BUF + T * MAXDPB];
-    float* ytile = smem + 2 * BUF;
+    // LDS: two staging buffers {x, dt, z: T x DPB; bc: T x 2N}, partial sums T x DPB x G
+    constexpr int BUF = 3 * T * DPB + T * 2 * N;
+    __shared__ __attribute__((aligned(16))) float smem[2 * BUF + T * DPB * (VASR_SCAN_DPP ? 1 : G)];
+    float* ypart = smem + 2 * BUF;
 
-    const int b = blockIdx.y;
-    const int d0 = blockIdx.x * DPB;
+    // XCD-aware block mapping: blocks id, id+8, id+16, ... share an XCD; give each such
+    // group consecutive (b, channel-block) work items so one utterance stays on one L2.
+    const int nd = Di / DPB;
+    const int nblk = B * nd;
+    const int id = blockIdx.x;
+    const int q8 = nblk / 8, r8 = nblk % 8, xg = id % 8;
+    const int wid = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + id / 8;
+    const int b = wid / nd;
+    const int d0 = (wid - b * nd) * DPB;
+
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int g = lane % G;
     const int dl = wave * DPW + lane / G;
 
-    float A2[NPL];
+    f2 A2[NP];
 #pragma unroll
-    for (int j = 0; j < NPL; ++j) A2[j] = A2g[g * NPL + j];
+    for (int p = 0; p < NP; ++p) A2[p] = f2{A2g[g * NPL + 2 * p], A2g[g * NPL + 2 * p + 1]};
 
     const int64_t row0 = (int64_t)b * L;
-    constexpr int q_xzd = T * DPB / 4;      // float4 per x/z/dt slab
-    constexpr int q_bc = T * 2 * N / 4;
-    constexpr int q_total = 3 * q_xzd + q_bc;
-    constexpr int nthreads = 64 * NW;
-    constexpr int MAXQ = (q_total + nthreads - 1) / nthreads;
-    float4 pre[MAXQ];
-
-    auto load_chunk = [&](int t0) {
-#pragma unroll
-        for (int k = 0; k < MAXQ; ++k) {
-            const int q = tid + k * nthreads;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (q < q_total) {
-                if (q < 3 * q_xzd) {
-                    const int arr = q / q_xzd, rem = q - arr * q_xzd;
-                    const int t = rem / (DPB / 4), c = (rem - t * (DPB / 4)) * 4;
-                    if (t0 + t < L) {
-                        const int64_t row = row0 + t0 + t;
-                        const float* src = arr == 0 ? xz + row * ld_xz + d0 + c
-                                         : arr == 1 ? dt + row * ld_dt + d0 + c
-                                                    : xz + row * ld_xz + Di + d0 + c;
-                        v = *reinterpret_cast<const float4*>(src);
-                    }
-                } else {
-                    const int rem = q - 3 * q_xzd;
-                    const int t = rem / (2 * N / 4), c = (rem - t * (2 * N / 4)) * 4;
-                    if (t0 + t < L) v = *reinterpret_cast<const float4*>(bc + (row0 + t0 + t) * ld_bc + c);
-                }
+    // Chunk staging by LDS-DMA (global_load_lds_dwordx4): each wave-instruction moves 1 KiB
+    // into a lane-linear LDS range; slabs x | dt | z (T x DPB) and bc (T x 2N) are
+    // contiguous, so instruction k of a chunk covers floats [256k, 256k + 256) of the buffer.
+    constexpr int SLAB = T * DPB;
+    constexpr int NINSTR = BUF / 256;
+    static_assert(BUF % 256 == 0 && SLAB % 256 == 0, "staging buffer must be whole 1-KiB pieces");
+    auto load_chunk = [&](int t0, float* buf) {
+        for (int k = wave; k < NINSTR; k += NW) {
+            const int off = k * 256 + lane * 4;  // float offset inside the buffer
+            const float* src;
+            if (off < 3 * SLAB) {
+                const int arr = off / SLAB, rem = off - arr * SLAB;
+                const int t = rem / DPB, c = rem - t * DPB;
+                const int64_t row = row0 + min(t0 + t, L - 1);
+                src = arr == 0 ? xz + row * ld_xz + d0 + c
+                    : arr == 1 ? dt + row * ld_dt + d0 + c
+                               : xz + row * ld_xz + Di + d0 + c;
+            } else {
+                const int rem = off - 3 * SLAB;
+                const int t = rem / (2 * N), c = rem - t * (2 * N);
+                src = bc + (row0 + min(t0 + t, L - 1)) * ld_bc + c;
             }
-            pre[k] = v;
-        }
-    };
-    auto store_chunk = [&](float* buf) {
-#pragma unroll
-        for (int k = 0; k < MAXQ; ++k) {
-            const int q = tid + k * nthreads;
-            if (q < q_total) {
-                float* dst;
-                if (q < 3 * q_xzd) {
-                    const int arr = q / q_xzd, rem = q - arr * q_xzd;
-                    const int t = rem / (DPB / 4), c = (rem - t * (DPB / 4)) * 4;
-                    dst = buf + arr * T * MAXDPB + t * DPB + c;
-                } else {
-                    const int rem = q - 3 * q_xzd;
-                    dst = buf + 3 * T * MAXDPB + rem * 4;
-                }
-                *reinterpret_cast<float4*>(dst) = pre[k];
-            }
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                             (lds_void*)(buf + k * 256), 16, 0, 0);
         }
     };
 
     const int nchunks = (L + T - 1) / T;
-    load_chunk(0);
-    store_chunk(smem);
+    load_chunk(0, smem);
     __syncthreads();
+    const float Dd = Dg[d0 + tid % DPB];
 
     TreeState<MAXUP> st;
-    float h[NPL];
+    f2 h[NP];
 #pragma unroll
-    for (int n = 0; n < NPL; ++n) {
-        st.pa[n] = 1.0f;
-        st.pb[n] = 0.0f;
-        h[n] = 0.0f;
+    for (int p = 0; p < NP; ++p) {
+        st.pa[p] = f2{1.0f, 1.0f};
+        st.pb[p] = f2{0.0f, 0.0f};
+        h[p] = f2{0.0f, 0.0f};
     }
 
     for (int c = 0; c < nchunks; ++c) {
         float* buf = smem + (c & 1) * BUF;
-        const float* xs = buf;
-        const float* dts = buf + T * MAXDPB;
-        const float* zs = buf + 2 * T * MAXDPB;
-        const float* bcs = buf + 3 * T * MAXDPB;
+        Smem sm{buf, buf + T * DPB, buf + 3 * T * DPB, ypart};
+        const float* zs = buf + 2 * T * DPB;
         const int t0 = c * T;
         const int nvalid = min(T, L - t0);
-        if (c + 1 < nchunks) load_chunk(t0 + T);
+        if (c + 1 < nchunks && !((VASR_SCAN_ABLATE & 8) && c > 0)) load_chunk(t0 + T, smem + ((c + 1) & 1) * BUF);
 
         if constexpr (MODE == 0) {
-            float cha[NPL], chb[NPL];
-            TreeChunk<0, MAXUP, G>::run(st, A2, nvalid, xs, dts, bcs, ytile, dl, g, DPB, N, cha, chb);
+            f2 cha[NP], chb[NP];
+            const StepIn first = load_step<0, N, DPB>(sm, dl, g);
+            if (nvalid == T)
+                TreeChunk<0, MAXUP, N, DPB, true>::run(st, sm, first, A2, dl, g, nvalid, cha, chb);
+            else
+                TreeChunk<0, MAXUP, N, DPB, false>::run(st, sm, first, A2, dl, g, nvalid, cha, chb);
             if (c + 1 < nchunks) merge_upper<MAXUP>(st, cha, chb, c);
         } else {
             for (int i = 0; i < nvalid; ++i) {
-                const float xv = xs[i * DPB + dl];
-                const float dv = dts[i * DPB + dl];
-                const float4 bv = *reinterpret_cast<const float4*>(bcs + i * 2 * N + g * NPL);
-                const float4 cv = *reinterpret_cast<const float4*>(bcs + i * 2 * N + N + g * NPL);
-                const float Bn[4] = {bv.x, bv.y, bv.z, bv.w};
-                const float Cn[4] = {cv.x, cv.y, cv.z, cv.w};
-                float part = 0.f;
+                const float xv = sm.xs[i * DPB + dl];
+                const float dv = sm.dts[i * DPB + dl];
+                const float4 bv = *reinterpret_cast<const float4*>(sm.bcs + i * 2 * N + g * NPL);
+                const float4 cv = *reinterpret_cast<const float4*>(sm.bcs + i * 2 * N + N + g * NPL);
+                const f2 Bn[NP] = {{bv.x, bv.y}, {bv.z, bv.w}};
+                const f2 Cn[NP] = {{cv.x, cv.y}, {cv.z, cv.w}};
+                const f2 dv2 = {dv, dv}, xv2 = {xv, xv};
+                f2 part = {0.f, 0.f};
 #pragma unroll
-                for (int n = 0; n < NPL; ++n) {
-                    const float dA = __builtin_amdgcn_exp2f(dv * A2[n]);
-                    const float dB = dv * Bn[n];
-                    h[n] = dA * h[n] + xv * dB;
-                    part = __builtin_fmaf(h[n], Cn[n], part);
+                for (int p = 0; p < NP; ++p) {
+                    const f2 dA = exp2v(dv2 * A2[p]);
+                    const f2 dB = dv2 * Bn[p];
+                    h[p] = dA * h[p] + xv2 * dB;
+                    part = part + h[p] * Cn[p];
                 }
-                part = group_sum<G>(part);
-                if (g == 0) ytile[i * DPB + dl] = part;
+                if constexpr (VASR_SCAN_DPP) {
+                    const float y = group_sum<G>(part.x + part.y);
+                    if (g == 0) ypart[i * DPB + dl] = y;
+                } else {
+                    ypart[(i * DPB + dl) * G + g] = part.x + part.y;
+                }
             }
         }
         __syncthreads();
-        // gated output of this chunk: (y + x D) * silu(z), coalesced along d
-        for (int idx = tid; idx < T * DPB; idx += nthreads) {
+        // gated output of this chunk: (sum_g partials + x D) * silu(z), coalesced along d
+        for (int idx = tid; idx < T * DPB; idx += 64 * NW) {
             const int t = idx / DPB, d = idx - t * DPB;
             if (t < nvalid) {
-                const float xv = xs[t * DPB + d];
+                float ysum;
+                if constexpr (VASR_SCAN_DPP) {
+                    ysum = ypart[t * DPB + d];
+                } else {
+                    const float4* pp = reinterpret_cast<const float4*>(ypart + (t * DPB + d) * G);
+                    float4 acc = pp[0];
+#pragma unroll
+                    for (int k = 1; k < G / 4; ++k) {
+                        const float4 v = pp[k];
+                        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+                    }
+                    ysum = (acc.x + acc.y) + (acc.z + acc.w);
+                }
+                const float xv = sm.xs[t * DPB + d];
                 const float zv = zs[t * DPB + d];
-                const float y = ytile[t * DPB + d] + xv * Dg[d0 + d];
+                const float y = ysum + xv * Dd;
                 const float silu = zv / (1.0f + expf(-zv));
                 out[(row0 + t0 + t) * ld_out + d0 + d] = y * silu;
             }
         }
-        if (c + 1 < nchunks) store_chunk(smem + ((c + 1) & 1) * BUF);
-        __syncthreads();
+        __syncthreads();  // also drains this wave's LDS-DMA of chunk c+1 (vmcnt(0) before the barrier)
     }
 }
 
@@ -331,24 +388,23 @@ template <int N, int MODE>
 int launch_n(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt, const float* bc, int64_t ld_bc,
              const float* A2, const float* D, float* out, int64_t ld_out, int B, int L, int Di, hipStream_t s) {
     constexpr int G = N / NPL;
-    constexpr int DPW = 64 / G;
-    constexpr int nw = 4;
-    if (Di % (nw * DPW) != 0) {
-        set_error("vasr_ssm_scan_f32: Di=%d must be a multiple of %d for N=%d", Di, nw * DPW, N);
+    constexpr int DPB = NW * (64 / G);
+    if (Di % DPB != 0) {
+        set_error("vasr_ssm_scan_f32: Di=%d must be a multiple of %d for N=%d", Di, DPB, N);
         return VASR_EUNSUPPORTED;
     }
-    dim3 grid(Di / (nw * DPW), B);
-    dim3 block(64 * nw);
+    dim3 grid(B * (Di / DPB));
+    dim3 block(64 * NW);
     const int nchunks = (L + T - 1) / T;
     if (MODE == 1 || nchunks <= 32)
         hipLaunchKernelGGL((ssm_scan_kernel<N, MODE, 5>), grid, block, 0, s, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D,
-                           out, ld_out, L, Di);
+                           out, ld_out, B, L, Di);
     else if (nchunks <= 128)
         hipLaunchKernelGGL((ssm_scan_kernel<N, MODE, 7>), grid, block, 0, s, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D,
-                           out, ld_out, L, Di);
+                           out, ld_out, B, L, Di);
     else
         hipLaunchKernelGGL((ssm_scan_kernel<N, MODE, 9>), grid, block, 0, s, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D,
-                           out, ld_out, L, Di);
+                           out, ld_out, B, L, Di);
     return launch_status("vasr_ssm_scan_f32");
 }
 
