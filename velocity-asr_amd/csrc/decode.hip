@@ -40,30 +40,43 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ x
     if (lane == 0) out[row] = bi < V ? bi : 0;
 }
 
-__global__ void collapse_kernel(const int32_t* __restrict__ pred, int B, int L, int blank, int collapse,
-                                int32_t* __restrict__ toks, int32_t* __restrict__ lens, int32_t* __restrict__ st,
-                                int32_t* __restrict__ en) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+// One wave per utterance, 64 frames per iteration.  A frame t is kept iff it is not blank
+// and (collapse == 0 or t == 0 or pred[t-1] != pred[t]) -- equivalent to the reference's
+// prev-token loop, since prev is None after a blank and equals pred[t-1] otherwise.  Kept
+// frames are compacted with a ballot + popcount prefix.  A kept token's end frame is the
+// next run start (the first frame whose value differs), matching decode.py:89-123.
+__global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict__ pred, int L, int blank, int collapse,
+                                                      int32_t* __restrict__ toks, int32_t* __restrict__ lens,
+                                                      int32_t* __restrict__ st, int32_t* __restrict__ en) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
     const int32_t* p = pred + (int64_t)b * L;
     int32_t* o = toks + (int64_t)b * L;
-    int n = 0;
-    int prev = -1;  // "None"
-    for (int t = 0; t < L; ++t) {
-        const int tok = p[t];
-        if (tok == blank) {
-            if (st && prev != -1 && prev != blank) en[(int64_t)b * L + n - 1] = t;
-            prev = st ? tok : -1;
-            continue;
+    int base = 0;  // tokens kept before this window
+    for (int t0 = 0; t0 < L; t0 += 64) {
+        const int t = t0 + lane;
+        const bool in = t < L;
+        const int tok = in ? p[t] : blank;
+        const int prv = (in && t > 0) ? p[t - 1] : -1;
+        const bool keep = in && tok != blank && (!collapse || t == 0 || prv != tok);
+        const unsigned long long kmask = __ballot(keep);
+        const int before = __popcll(kmask & ((1ull << lane) - 1ull));
+        if (keep) {
+            o[base + before] = tok;
+            if (st) st[(int64_t)b * L + base + before] = t;
         }
-        if (collapse && tok == prev) continue;
-        if (st && prev != -1 && prev != blank) en[(int64_t)b * L + n - 1] = t;
-        if (st) st[(int64_t)b * L + n] = t;
-        o[n++] = tok;
-        prev = tok;
+        if (st) {
+            // a run starting at t closes the previous run; if that run was a kept token, it is
+            // the last token kept before t
+            const bool run_start = in && t > 0 && prv != tok && prv != blank;
+            if (run_start) en[(int64_t)b * L + base + before - 1] = t;
+        }
+        base += __popcll(kmask);
     }
-    if (st && prev != -1 && prev != blank) en[(int64_t)b * L + n - 1] = L;
-    lens[b] = n;
+    if (lane == 0) {
+        lens[b] = base;
+        if (st && L > 0 && p[L - 1] != blank && base > 0) en[(int64_t)b * L + base - 1] = L;
+    }
 }
 
 }  // namespace
@@ -86,7 +99,7 @@ VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int
     VASR_CHECK_ARG(out_start == nullptr || collapse, "vasr_ctc_collapse: timestamps need collapse=1");
     VASR_CHECK_ARG(B >= 0 && L >= 0, "vasr_ctc_collapse: bad shape");
     if (B == 0) return VASR_OK;
-    hipLaunchKernelGGL(collapse_kernel, dim3((B + 63) / 64), dim3(64), 0, as_stream(stream), pred, B, L, blank, collapse,
-                       out_tokens, out_len, out_start, out_end);
+    hipLaunchKernelGGL(collapse_kernel, dim3(B), dim3(64), 0, as_stream(stream), pred, L, blank, collapse, out_tokens,
+                       out_len, out_start, out_end);
     return launch_status("vasr_ctc_collapse");
 }

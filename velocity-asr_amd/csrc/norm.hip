@@ -48,10 +48,13 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
     ln_row_to(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
 }
 
-constexpr int TT = 32;       // output rows per block
+constexpr int TT = 64;       // output rows per block
 constexpr int kMaxC = 256;   // LDS row capacity
 constexpr int kMaxK = 8;
 
+// Phase 1: the 4 waves layer-norm rows t0-(Kc-1) .. t0+TT-1 into LDS (zero rows before t=0).
+// Phase 2: thread c owns channel c for all TT rows: taps and bias in registers, a sliding
+// window of the last Kc LN values, one LDS read and one coalesced store per output.
 __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b,
@@ -62,12 +65,12 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * TT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nrows = TT + Kc - 1;
+    const int nrows = min(TT, L - t0) + Kc - 1;
     const float* xb = x + (int64_t)b * L * C;
     for (int rr = wave; rr < nrows; rr += 4) {
         const int t = t0 - (Kc - 1) + rr;
-        float* dst = tile + rr * kMaxC;
-        if (t < 0 || t >= L) {
+        float* dst = tile + rr * C;
+        if (t < 0) {
             for (int c = lane; c < C; c += 64) dst[c] = 0.f;  // causal zero padding
         } else {
             ln_row_to(xb + (int64_t)t * C, ln_w, ln_b, dst, C, eps, lane);
@@ -75,13 +78,31 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     }
     __syncthreads();
     float* yb = y + (int64_t)b * L * C;
-    for (int idx = threadIdx.x; idx < TT * C; idx += 256) {
-        const int tt = idx / C, c = idx - tt * C;
-        const int t = t0 + tt;
-        if (t >= L) break;
-        float acc = 0.f;
-        for (int j = 0; j < Kc; ++j) acc += tile[(tt + j) * kMaxC + c] * cw[c * Kc + j];
-        yb[(int64_t)t * C + c] = acc + cb[c];
+    const int rows = min(TT, L - t0);
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float w[kMaxK], win[kMaxK];
+#pragma unroll
+        for (int j = 0; j < kMaxK; ++j) {
+            w[j] = j < Kc ? cw[c * Kc + j] : 0.f;
+            win[j] = (j < Kc - 1) ? tile[j * C + c] : 0.f;
+        }
+        const float bias = cb[c];
+        for (int tt = 0; tt < rows; ++tt) {
+            // window = LN rows tt .. tt + Kc - 1 of the tile (inputs t - Kc + 1 .. t)
+            const float v = tile[(tt + Kc - 1) * C + c];
+            float acc = 0.f;
+#pragma unroll
+            for (int j = 0; j < kMaxK; ++j) {
+                if (j < Kc - 1) acc += win[j] * w[j];
+                else if (j == Kc - 1) acc += v * w[j];
+            }
+#pragma unroll
+            for (int j = 0; j + 1 < kMaxK; ++j) {
+                if (j < Kc - 2) win[j] = win[j + 1];
+                else if (j == Kc - 2) win[j] = v;
+            }
+            yb[(int64_t)(t0 + tt) * C + c] = acc + bias;
+        }
     }
 }
 

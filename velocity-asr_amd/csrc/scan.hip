@@ -116,16 +116,35 @@ __device__ __forceinline__ f2 exp2v(f2 v) {
     return r;
 }
 
+// The state-independent part of a step: dA = exp2(dt A2), dBx = x (dt B), and C.
+struct StepElem {
+    f2 a[NP], b[NP];
+    float4 cv;
+};
+
+__device__ __forceinline__ StepElem make_elem(const StepIn& in, const f2 (&A2)[NP]) {
+#pragma clang fp contract(off)
+    StepElem e;
+    const f2 dt2 = {in.dt, in.dt};
+    const f2 x2 = {in.x, in.x};
+    const f2 Bn[NP] = {{in.bv.x, in.bv.y}, {in.bv.z, in.bv.w}};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        e.a[p] = (VASR_SCAN_ABLATE & 1) ? dt2 * A2[p] : exp2v(dt2 * A2[p]);
+        const f2 dB = dt2 * Bn[p];
+        e.b[p] = x2 * dB;
+    }
+    e.cv = in.cv;
+    return e;
+}
+
 // One push of the streaming tree scan at in-chunk step I; stores this lane's partial y.
 template <int I, int MAXUP, int N, int DPB>
-__device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, const StepIn& in, const f2 (&A2)[NP],
-                                          int dl, int g, f2 (&chunk_a)[NP], f2 (&chunk_b)[NP]) {
+__device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, const StepElem& el, int dl, int g,
+                                          f2 (&chunk_a)[NP], f2 (&chunk_b)[NP]) {
 #pragma clang fp contract(off)
     constexpr int G = N / NPL;
-    const float x = in.x;
-    const float dt = in.dt;
-    const f2 Bn[NP] = {{in.bv.x, in.bv.y}, {in.bv.z, in.bv.w}};
-    const f2 Cn[NP] = {{in.cv.x, in.cv.y}, {in.cv.z, in.cv.w}};
+    const f2 Cn[NP] = {{el.cv.x, el.cv.y}, {el.cv.z, el.cv.w}};
     // y contribution of h[t] (the exclusive prefix = cb of the current top block)
     f2 part;
 #pragma unroll
@@ -145,13 +164,10 @@ __device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, c
     }
 
     constexpr int J = trailing_ones(I);
-    const f2 dt2 = {dt, dt};
-    const f2 x2 = {x, x};
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-        f2 cur_a = (VASR_SCAN_ABLATE & 1) ? dt2 * A2[p] : exp2v(dt2 * A2[p]);
-        const f2 dB = dt2 * Bn[p];
-        f2 cur_b = x2 * dB;
+        f2 cur_a = el.a[p];
+        f2 cur_b = el.b[p];
 #pragma unroll
         for (int k = 0; k < J; ++k) {  // up-sweep: (a_r, b_r) <- (a_r a_l, a_r b_l + b_r)
             cur_b = cur_a * s.lb[k][p] + cur_b;
@@ -217,23 +233,28 @@ __device__ __forceinline__ void merge_upper(TreeState<MAXUP>& s, const f2 (&chun
     }
 }
 
+// Two-stage software pipeline over the chunk's 16 steps: operands of step I+2 are read from
+// LDS and the state-independent part of step I+1 (exp2, dB, x*dB) is computed while step I's
+// tree update runs, so the LDS and v_exp latencies overlap the dependent tree arithmetic.
 template <int I, int MAXUP, int N, int DPB, bool FULL>
 struct TreeChunk {
-    __device__ __forceinline__ static void run(TreeState<MAXUP>& s, const Smem& sm, const StepIn& cur,
-                                               const f2 (&A2)[NP], int dl, int g, int nvalid, f2 (&ca)[NP],
-                                               f2 (&cb)[NP]) {
+    __device__ __forceinline__ static void run(TreeState<MAXUP>& s, const Smem& sm, const StepIn& raw_next,
+                                               const StepElem& el, const f2 (&A2)[NP], int dl, int g, int nvalid,
+                                               f2 (&ca)[NP], f2 (&cb)[NP]) {
         if (FULL || I < nvalid) {
-            StepIn nxt;
-            if constexpr (I + 1 < T) nxt = load_step<I + 1, N, DPB>(sm, dl, g);  // one step ahead
-            tree_step<I, MAXUP, N, DPB>(s, sm, cur, A2, dl, g, ca, cb);
-            TreeChunk<I + 1, MAXUP, N, DPB, FULL>::run(s, sm, nxt, A2, dl, g, nvalid, ca, cb);
+            StepIn raw2;
+            if constexpr (I + 2 < T) raw2 = load_step<I + 2, N, DPB>(sm, dl, g);
+            StepElem el_next;
+            if constexpr (I + 1 < T) el_next = make_elem(raw_next, A2);
+            tree_step<I, MAXUP, N, DPB>(s, sm, el, dl, g, ca, cb);
+            TreeChunk<I + 1, MAXUP, N, DPB, FULL>::run(s, sm, raw2, el_next, A2, dl, g, nvalid, ca, cb);
         }
     }
 };
 template <int MAXUP, int N, int DPB, bool FULL>
 struct TreeChunk<T, MAXUP, N, DPB, FULL> {
-    __device__ __forceinline__ static void run(TreeState<MAXUP>&, const Smem&, const StepIn&, const f2 (&)[NP], int,
-                                               int, int, f2 (&)[NP], f2 (&)[NP]) {}
+    __device__ __forceinline__ static void run(TreeState<MAXUP>&, const Smem&, const StepIn&, const StepElem&,
+                                               const f2 (&)[NP], int, int, int, f2 (&)[NP], f2 (&)[NP]) {}
 };
 
 template <int N, int MODE, int MAXUP>
@@ -324,11 +345,13 @@ __global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const fl
 
         if constexpr (MODE == 0) {
             f2 cha[NP], chb[NP];
-            const StepIn first = load_step<0, N, DPB>(sm, dl, g);
+            const StepIn r0 = load_step<0, N, DPB>(sm, dl, g);
+            const StepIn r1 = load_step<1, N, DPB>(sm, dl, g);
+            const StepElem e0 = make_elem(r0, A2);
             if (nvalid == T)
-                TreeChunk<0, MAXUP, N, DPB, true>::run(st, sm, first, A2, dl, g, nvalid, cha, chb);
+                TreeChunk<0, MAXUP, N, DPB, true>::run(st, sm, r1, e0, A2, dl, g, nvalid, cha, chb);
             else
-                TreeChunk<0, MAXUP, N, DPB, false>::run(st, sm, first, A2, dl, g, nvalid, cha, chb);
+                TreeChunk<0, MAXUP, N, DPB, false>::run(st, sm, r1, e0, A2, dl, g, nvalid, cha, chb);
             if (c + 1 < nchunks) merge_upper<MAXUP>(st, cha, chb, c);
         } else {
             for (int i = 0; i < nvalid; ++i) {
