@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=1, help="utterance groups replayed on concurrent HIP streams")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -140,7 +141,7 @@ def main():
         def step():
             return audio_to_token_ids(model, audio)
     else:
-        tr = GraphedTranscriber(model, B, S_len, dev)
+        tr = GraphedTranscriber(model, B, S_len, dev, streams=args.streams)
         tr.audio.copy_(audio)
         step = tr.step
 
@@ -215,7 +216,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic: N(0, 0.1) 16 kHz clips; seeded random-init weights (velocity_asr.synthetic)",
         "config": {"workload": f"{B} x {args.seconds:g} s clips per GPU, audio->mel->forward->CTC greedy tokens "
-                               f"(BASELINE configs[1]{', HIP graph' if not args.eager else ', eager'})",
+                               f"(BASELINE configs[1]{f', HIP graph x{args.streams} streams' if not args.eager else ', eager'})",
                    "global_batch": world * B, "clip_seconds": args.seconds, "parallelism": f"utterance-shard x{world}"},
         "frames_per_sec": round(frames / elapsed, 1),
         "roofline": roof,

@@ -34,27 +34,60 @@ def token_lists(toks: torch.Tensor, lens: torch.Tensor) -> List[List[int]]:
 
 
 class GraphedTranscriber:
-    """Fixed-shape (B, S) audio -> tokens step captured once in a HIP graph.
+    """Fixed-shape (B, S) audio -> tokens step captured once in HIP graphs.
 
     ``audio`` is the static input buffer (write new clips into it, or use it as-is for
-    resident benchmark inputs); ``step()`` replays the graph; ``tokens`` / ``lengths``
-    are the static outputs.
+    resident benchmark inputs); ``step()`` replays; ``tokens`` / ``lengths`` are the static
+    outputs.  With ``streams > 1`` the batch is split into that many utterance groups, each
+    captured in its own graph and replayed on its own HIP stream: the groups are independent
+    (no padding masks, per-utterance statistics), so results are bitwise those of one graph,
+    while the VALU-bound scan of one group overlaps the MFMA-bound GEMMs of another on the
+    same CUs (separate pipes).
     """
 
     def __init__(self, model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
-                 warmup: int = 2):
+                 warmup: int = 2, streams: int = 1):
         self.model = model
         dev = device or next(model.parameters()).device
+        self.device = dev
+        if batch % streams:
+            raise ValueError("batch must divide by the number of streams")
         self.audio = torch.zeros((batch, samples), device=dev, dtype=torch.float32)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(warmup):  # builds the cached weight layouts before capture
-                audio_to_token_ids(model, self.audio)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.tokens, self.lengths = audio_to_token_ids(model, self.audio)
+        g = batch // streams
+        self.streams = [torch.cuda.Stream(dev) for _ in range(streams)]
+        views = [self.audio[i * g:(i + 1) * g] for i in range(streams)]
+        main = torch.cuda.current_stream(dev)
+        for st, v in zip(self.streams, views):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                for _ in range(warmup):  # builds the cached weight layouts before capture
+                    audio_to_token_ids(model, v)
+            main.wait_stream(st)
+        self.graphs = []
+        outs = []
+        for st, v in zip(self.streams, views):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=st):
+                outs.append(audio_to_token_ids(model, v))
+            self.graphs.append(gr)
+        self.group_outputs = outs
+        if streams == 1:
+            self.tokens, self.lengths = outs[0]
+        else:
+            self.tokens = torch.cat([o[0] for o in outs], 0)  # snapshot; refresh with collect()
+            self.lengths = torch.cat([o[1] for o in outs], 0)
 
     def step(self) -> None:
-        self.graph.replay()
+        main = torch.cuda.current_stream(self.device)
+        for st, gr in zip(self.streams, self.graphs):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                gr.replay()
+        for st in self.streams:
+            main.wait_stream(st)
+
+    def collect(self):
+        """(tokens, lengths) of the last step, concatenated over the stream groups."""
+        if len(self.graphs) == 1:
+            return self.tokens, self.lengths
+        return (torch.cat([o[0] for o in self.group_outputs], 0), torch.cat([o[1] for o in self.group_outputs], 0))
