@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 1
+#define VASR_ABI_VERSION 2
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -78,6 +78,20 @@ typedef struct vasr_gemm_args {
 } vasr_gemm_args;
 
 int vasr_linear_f32(const vasr_gemm_args* args, void* stream);
+
+/* The same GEMM (same args, epilogues and results to within fp32 accumulation order) on
+ * the bf16 matrix cores: fp32 operands are split exactly into three bf16 terms
+ * (x = hi + mid + lo, all 24 significant bits) and the six products larger than
+ * 2^-25 |a||b| are accumulated in fp32 on v_mfma_f32_32x32x16_bf16 — 2.67x the
+ * f32-input MFMA rate.  `w_split` holds W pre-split by vasr_split_weights_bf16x3
+ * (args->W is not read).  Replaces the same reference ops as vasr_linear_f32.
+ */
+int vasr_linear_x3_f32(const vasr_gemm_args* args, const uint16_t* w_split, void* stream);
+
+/* Split W (N x K fp32, row stride ldw) into bf16 planes out[3][N][Kp] (hi, mid, lo;
+ * Kp = K rounded up to 32, zero padded).  vasr_split_weights_elems(N, K) = 3*N*Kp. */
+int vasr_split_weights_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
+int64_t vasr_split_weights_elems(int N, int K);
 
 /* ------------------------------------------------------------------ norms / conv
  * nn.LayerNorm over the last dim (C <= 1024), biased variance.  y may alias x.

@@ -50,11 +50,20 @@ def t(x):
     return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
 
 
+@pytest.fixture(params=["x3", "f32"])
+def gemm_mode(request, va):
+    """Run a GEMM test with each engine: split-bf16 ("x3", the default) and f32-input MFMA."""
+    from velocity_asr import ops
+    prev = ops.set_gemm_mode(request.param)
+    yield request.param
+    ops.set_gemm_mode(prev)
+
+
 # ----------------------------------------------------------------------------- kernels
 @pytest.mark.parametrize("M,N,K", [(1, 64, 32), (33, 192, 192), (257, 768, 192), (300, 512, 384),
                                    (130, 1000, 192), (64, 48, 48), (5, 96, 240)])
 @pytest.mark.parametrize("epi", ["none", "gelu", "softplus", "residual"])
-def test_gemm_epilogues(va, M, N, K, epi):
+def test_gemm_epilogues(va, gemm_mode, M, N, K, epi):
     from velocity_asr import _lib, ops
     g = torch.Generator().manual_seed(M * 7 + N)
     a = torch.randn(M, K, generator=g)
@@ -81,7 +90,7 @@ def test_gemm_epilogues(va, M, N, K, epi):
     assert (out - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
 
-def test_gemm_strided_views_and_batches(va):
+def test_gemm_strided_views_and_batches(va, gemm_mode):
     from velocity_asr import ops
     g = torch.Generator().manual_seed(3)
     big = torch.randn(50, 100, generator=g).to(DEV)
@@ -97,6 +106,44 @@ def test_gemm_strided_views_and_batches(va):
     rows = torch.stack([torch.stack([base[b, 40 * m: 40 * m + 120] for m in range(20)]) for b in range(3)])
     ref = rows.double() @ wb.double().T
     assert (res.cpu().double() - ref).abs().max().item() < 1e-4
+
+
+def test_gemm_x3_accuracy_matches_f32(va):
+    """Split-bf16 GEMM error vs fp64 stays at the f32-MFMA GEMM's level, also for operands
+    spanning 2^-20..2^20 (the split keeps all 24 bits of every value)."""
+    from velocity_asr import ops
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 512, 384, 768
+    for scale in (False, True):
+        a = torch.randn(M, K, generator=g)
+        w = torch.randn(N, K, generator=g) / K ** 0.5
+        if scale:
+            a = a * torch.exp2(torch.randint(-20, 21, (M, K), generator=g).float())
+            w = w * torch.exp2(torch.randint(-20, 21, (N, K), generator=g).float())
+        ref = a.double() @ w.double().T
+        bound = (a.double().abs() @ w.double().abs().T)  # condition-aware error scale
+        errs = {}
+        for mode in ("x3", "f32"):
+            prev = ops.set_gemm_mode(mode)
+            try:
+                out = ops.gemm(a.to(DEV), w.to(DEV)).cpu().double()
+            finally:
+                ops.set_gemm_mode(prev)
+            errs[mode] = ((out - ref).abs() / bound).max().item()
+        assert errs["f32"] < 2 ** -16
+        assert errs["x3"] < max(2.0 * errs["f32"], 2 ** -20), errs
+
+
+def test_split_weights_planes(va):
+    """hi + mid + lo reproduces every fp32 weight exactly; K padded with zeros."""
+    from velocity_asr import ops
+    g = torch.Generator().manual_seed(5)
+    w = (torch.randn(70, 100, generator=g) * torch.exp2(torch.randint(-30, 31, (70, 100), generator=g).float()))
+    planes = ops.split_weights(w.to(DEV)).cpu().view(3, 70, 128)
+    f = (planes.to(torch.int32) & 0xFFFF) << 16
+    vals = f.view(torch.float32).double()
+    np.testing.assert_array_equal(vals.sum(0)[:, :100].float().numpy(), w.numpy())
+    assert (planes[:, :, 100:] == 0).all()
 
 
 def test_layer_norm_and_dwconv(va):
@@ -267,7 +314,7 @@ def test_argmax_ties_first_index(va):
 
 
 # ----------------------------------------------------------------------------- model
-def test_forward_stages_b2_3s(va, model):
+def test_forward_stages_b2_3s(va, gemm_mode, model):
     g = golden("fwd_b2_3s.npz")
     logits, f = model(t(g["mel"]), return_features=True)
     np.testing.assert_allclose(f["temporal_binding"].cpu().numpy(), g["temporal_binding"], atol=1e-4, rtol=1e-4)
@@ -288,7 +335,7 @@ def test_audio_to_tokens_b2_3s(va, model):
     assert [[tk, [list(x) for x in s]] for tk, s in ts] == dec["b2_3s_ts"]
 
 
-def test_headline_shape_b2_10s(va, model):
+def test_headline_shape_b2_10s(va, gemm_mode, model):
     g = golden("fwd_b2_10s.npz")
     mel = va.compute_mel_spectrogram(t(S.make_audio(2, 160000, seed=1234)))
     logits = model(mel)

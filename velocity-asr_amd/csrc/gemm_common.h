@@ -1,0 +1,190 @@
+// Pieces shared by the two GEMM main loops (gemm_f32.hip: f32-input MFMA; gemm_x3.hip:
+// split-bf16 MFMA): parameters, the XCD-aware tile decode, the fused epilogues and the
+// tile-configuration cost model.  Both main loops leave the same accumulator layout —
+// the 32x32 C/D map is dtype-independent on gfx950 — so one epilogue serves both.
+#pragma once
+
+#include "vasr_internal.h"
+
+namespace vasr {
+namespace gemm {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+#ifndef VASR_GEMM_XCD
+#define VASR_GEMM_XCD 1   // XCD-aware tile order (diagnostic builds may turn it off)
+#endif
+
+struct GemmParams {
+    const float* A;
+    int64_t lda, stride_a;
+    const float* W;
+    int64_t ldw;
+    const uint16_t* Wx;  // split-bf16 planes [3][N][Kp] (gemm_x3 only)
+    int Kp;
+    const float* bias;
+    float* C;
+    int64_t ldc, stride_c;
+    int M, N, K;
+    const float* aux;
+    int64_t ld_aux, stride_aux;
+    const float* aux2;
+    int n_out;
+};
+
+struct Tile {
+    int bz, m0, n0;
+};
+
+// The grid is 1-D; blocks id, id + 8, id + 16, ... are dealt to the same XCD (round-robin
+// dispatch), so each such group gets a contiguous, M-major run of tiles: all N tiles of an
+// A row panel then run on one XCD and share its L2.
+template <int BM, int BN>
+__device__ __forceinline__ Tile decode_tile(const GemmParams& p) {
+    const int tiles_n = (p.N + BN - 1) / BN;
+    const int tiles_m = (p.M + BM - 1) / BM;
+    const int tiles = tiles_n * tiles_m * (int)gridDim.y;
+    int w = blockIdx.x + (int)blockIdx.y * (int)gridDim.x;
+    if (VASR_GEMM_XCD) {
+        const int q8 = tiles / 8, r8 = tiles % 8, xg = w % 8;
+        w = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + w / 8;
+    }
+    const int per_batch = tiles_n * tiles_m;
+    Tile t;
+    t.bz = w / per_batch;
+    const int wr_ = w - t.bz * per_batch;
+    t.m0 = (wr_ / tiles_n) * BM;
+    t.n0 = (wr_ % tiles_n) * BN;
+    return t;
+}
+
+// Accumulator element i of MFMA tile (tm, tn) of wave (wr, wc), lane (r, h) is
+// C[m0 + wr*32*TM + tm*32 + (i&3) + 8*(i>>2) + 4*h][n0 + wc*32*TN + tn*32 + r].
+//
+// The "pair" epilogues rely on the two 32-column MFMA tiles of a wave (tn = 0, 1) holding
+// two views of the same 32 output columns in the same lane and register: PAIR_POWER puts
+// DFT cos|sin rows side by side (|X|^2 in-register); PAIR_FUSION puts the gate and
+// global_proj rows side by side (gated fusion in-register).
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, floatx16 (&acc)[TM][TN], int wr,
+                                         int wc, int r, int h) {
+    float* __restrict__ Cb = p.C + (int64_t)t.bz * p.stride_c;
+    const float* __restrict__ auxb = p.aux ? p.aux + (int64_t)t.bz * p.stride_aux : nullptr;
+    const int m0 = t.m0, n0 = t.n0;
+
+    if constexpr (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) {
+        const int col = (n0 + wc * 32 * TN) / 2 + r;  // output column of this lane
+        if (col >= p.n_out) return;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (row >= p.M) continue;
+                const float v0 = acc[tm][0][i];
+                const float v1 = acc[tm][TN - 1][i];
+                float out;
+                if constexpr (EPI == VASR_EPI_PAIR_POWER) {
+                    out = v0 * v0 + v1 * v1;
+                } else {
+                    // aux: local-side partial products in the same paired layout.
+                    const int pc = n0 + wc * 32 * TN + r;  // paired column of half 0
+                    const float* ar = auxb + (int64_t)row * p.ld_aux;
+                    const float gate = sigmoidf_((ar[pc] + v0) + p.bias[pc]);
+                    const float lt = ar[pc + 32] + p.aux2[col];
+                    const float gt = v1 + p.bias[pc + 32];
+                    out = gate * lt + (1.0f - gate) * gt;
+                }
+                Cb[(int64_t)row * p.ldc + col] = out;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) {
+                const int col = n0 + wc * 32 * TN + tn * 32 + r;
+                if (col >= p.N) continue;
+                const float bv = p.bias ? p.bias[col] : 0.0f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (row >= p.M) continue;
+                    float v = acc[tm][tn][i];
+                    if (p.bias) v = v + bv;
+                    if constexpr (EPI == VASR_EPI_GELU) {
+                        v = gelu_erf(v);
+                    } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
+                        if (col >= p.n_out) v = softplus20(v);
+                    } else if constexpr (EPI == VASR_EPI_RESIDUAL) {
+                        v = v + auxb[(int64_t)row * p.ld_aux + col];
+                    } else if constexpr (EPI == VASR_EPI_GELU_PE) {
+                        v = gelu_erf(v) + auxb[(int64_t)row * p.ld_aux + col];
+                    }
+                    Cb[(int64_t)row * p.ldc + col] = v;
+                }
+            }
+        }
+    }
+}
+
+// Tile configurations: {WM, WN, TM, TN, blocks per CU the kernel's VGPR/LDS use admits}.
+struct TileCfg {
+    int wm, wn, tm, tn, occ;
+    int bm() const { return wm * 32 * tm; }
+    int bn() const { return wn * 32 * tn; }
+};
+constexpr int kCUs = 256;
+
+// Pick the tile that minimises (rounds of resident blocks) x (blocks sharing a CU) x tile area:
+// at M = 16032 the grids are only one or two rounds deep, so wave quantisation and CU
+// balance, not per-tile efficiency, decide the time (measured in tools/gemm_variants_run.py).
+inline int pick_cfg(const TileCfg* cfgs, int n, int M, int N, int batch, bool pair) {
+    int best = -1;
+    double best_cost = 0;
+    for (int i = 0; i < n; ++i) {
+        const TileCfg& c = cfgs[i];
+        if (pair && c.tn != 2) continue;
+        const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
+        const long per_cu = (tiles + kCUs - 1) / kCUs;
+        const long rounds = (per_cu + c.occ - 1) / c.occ;
+        const double cost = (double)rounds * (double)(per_cu < c.occ ? per_cu : c.occ) * c.bm() * c.bn();
+        if (best < 0 || cost < best_cost * 0.999) {
+            best = i;
+            best_cost = cost;
+        }
+    }
+    return best;
+}
+
+// Argument checks common to both GEMM entry points; fills p (W / Wx left to the caller).
+inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
+    VASR_CHECK_ARG(a != nullptr, "%s: null args", fn);
+    VASR_CHECK_ARG(a->A && a->C, "%s: null A/C", fn);
+    VASR_CHECK_ARG(a->M >= 0 && a->N > 0 && a->K > 0 && a->batch >= 1, "%s: bad shape M=%d N=%d K=%d batch=%d", fn,
+                   a->M, a->N, a->K, a->batch);
+    VASR_CHECK_ARG(a->K % 4 == 0 && a->lda % 4 == 0 && a->stride_a % 4 == 0,
+                   "%s: K, lda, stride_a must be multiples of 4 (K=%d lda=%lld)", fn, a->K, (long long)a->lda);
+    VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->A) & 15) == 0, "%s: A must be 16-byte aligned", fn);
+    const int epi = a->epilogue;
+    VASR_CHECK_ARG(epi >= VASR_EPI_NONE && epi <= VASR_EPI_PAIR_FUSION, "%s: unknown epilogue %d", fn, epi);
+    const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
+    if (pair)
+        VASR_CHECK_ARG(a->N % 64 == 0 && a->n_out > 0 && a->n_out <= a->N / 2,
+                       "%s: paired epilogue needs N %% 64 == 0 and 0 < n_out <= N/2", fn);
+    if (epi == VASR_EPI_RESIDUAL || epi == VASR_EPI_GELU_PE || epi == VASR_EPI_PAIR_FUSION)
+        VASR_CHECK_ARG(a->aux != nullptr, "%s: epilogue %d needs aux", fn, epi);
+    if (epi == VASR_EPI_PAIR_FUSION)
+        VASR_CHECK_ARG(a->aux2 != nullptr && a->bias != nullptr, "%s: fusion needs bias and aux2", fn);
+    p.A = a->A; p.lda = a->lda; p.stride_a = a->stride_a;
+    p.W = a->W; p.ldw = a->ldw; p.Wx = nullptr; p.Kp = 0;
+    p.bias = a->bias;
+    p.C = a->C; p.ldc = a->ldc; p.stride_c = a->stride_c;
+    p.M = a->M; p.N = a->N; p.K = a->K;
+    p.aux = a->aux; p.ld_aux = a->ld_aux; p.stride_aux = a->stride_aux;
+    p.aux2 = a->aux2; p.n_out = a->n_out;
+    return VASR_OK;
+}
+
+}  // namespace gemm
+}  // namespace vasr

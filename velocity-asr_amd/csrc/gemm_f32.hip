@@ -9,39 +9,16 @@
 // every MFMA; over the 16 k-steps of a BK tile lane half h covers k = h*16 .. h*16+15,
 // so A and W fragments are read as contiguous float4s (ds_read_b128).  Rows are padded
 // to 36 floats: every ds_read_b128 lane group then hits 16 distinct 4-bank slots.
-//
-// The "pair" epilogues rely on the two 32-column MFMA tiles of a wave (tn = 0, 1)
-// holding two views of the same 32 output columns in the same lane and register:
-// PAIR_POWER puts DFT cos|sin rows side by side (|X|^2 in-register); PAIR_FUSION puts
-// the gate and global_proj rows side by side (gated fusion in-register).
-#include "vasr_internal.h"
+// Tile decode, epilogues and the tile cost model: gemm_common.h.
+#include "gemm_common.h"
 
 namespace vasr {
 namespace {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-#ifndef VASR_GEMM_XCD
-#define VASR_GEMM_XCD 1   // XCD-aware tile order (diagnostic builds may turn it off)
-#endif
+using namespace gemm;
 
 constexpr int BK = 32;
 constexpr int SK = BK + 4;  // padded LDS row (floats)
-
-struct GemmParams {
-    const float* A;
-    int64_t lda, stride_a;
-    const float* W;
-    int64_t ldw;
-    const float* bias;
-    float* C;
-    int64_t ldc, stride_c;
-    int M, N, K;
-    const float* aux;
-    int64_t ld_aux, stride_aux;
-    const float* aux2;
-    int n_out;
-};
 
 template <int WM, int WN, int TM, int TN, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
@@ -64,23 +41,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     const int r = lane & 31;
     const int h = lane >> 5;
 
-    // Tile decode.  The grid is 1-D; blocks id, id + 8, id + 16, ... are dealt to the same XCD
-    // (round-robin dispatch), so each such group gets a contiguous, M-major run of tiles: all
-    // N tiles of an A row panel then run on one XCD and share its L2.
-    const int tiles_n = (p.N + BN - 1) / BN;
-    const int tiles_m = (p.M + BM - 1) / BM;
-    const int tiles = tiles_n * tiles_m * (int)gridDim.y;
-    int w = blockIdx.x + (int)blockIdx.y * (int)gridDim.x;
-    if (VASR_GEMM_XCD) {
-        const int q8 = tiles / 8, r8 = tiles % 8, xg = w % 8;
-        w = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + w / 8;
-    }
-    const int per_batch = tiles_n * tiles_m;
-    const int bz = w / per_batch;
-    const int wr_ = w - bz * per_batch;
-    const int m0 = (wr_ / tiles_n) * BM;
-    const int n0 = (wr_ % tiles_n) * BN;
-    const float* __restrict__ A = p.A + (int64_t)bz * p.stride_a;
+    const Tile t = decode_tile<BM, BN>(p);
+    const int m0 = t.m0, n0 = t.n0;
+    const float* __restrict__ A = p.A + (int64_t)t.bz * p.stride_a;
     const float* __restrict__ W = p.W;
 
     float4 ra[A_LOADS], rw[W_LOADS];
@@ -167,64 +130,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         }
     }
 
-    // ---------------------------------------------------------------- epilogue
-    float* __restrict__ Cb = p.C + (int64_t)bz * p.stride_c;
-    const float* __restrict__ auxb = p.aux ? p.aux + (int64_t)bz * p.stride_aux : nullptr;
-
-    if constexpr (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) {
-        const int col = (n0 + wc * 32 * TN) / 2 + r;  // output column of this lane
-        if (col >= p.n_out) return;
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (row >= p.M) continue;
-                const float v0 = acc[tm][0][i];
-                const float v1 = acc[tm][TN - 1][i];
-                float out;
-                if constexpr (EPI == VASR_EPI_PAIR_POWER) {
-                    out = v0 * v0 + v1 * v1;
-                } else {
-                    // aux: local-side partial products in the same paired layout.
-                    const int pc = n0 + wc * 32 * TN + r;  // paired column of half 0
-                    const float* ar = auxb + (int64_t)row * p.ld_aux;
-                    const float gate = sigmoidf_((ar[pc] + v0) + p.bias[pc]);
-                    const float lt = ar[pc + 32] + p.aux2[col];
-                    const float gt = v1 + p.bias[pc + 32];
-                    out = gate * lt + (1.0f - gate) * gt;
-                }
-                Cb[(int64_t)row * p.ldc + col] = out;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) {
-                const int col = n0 + wc * 32 * TN + tn * 32 + r;
-                if (col >= p.N) continue;
-                const float bv = p.bias ? p.bias[col] : 0.0f;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    if (row >= p.M) continue;
-                    float v = acc[tm][tn][i];
-                    if (p.bias) v = v + bv;
-                    if constexpr (EPI == VASR_EPI_GELU) {
-                        v = gelu_erf(v);
-                    } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
-                        if (col >= p.n_out) v = softplus20(v);
-                    } else if constexpr (EPI == VASR_EPI_RESIDUAL) {
-                        v = v + auxb[(int64_t)row * p.ld_aux + col];
-                    } else if constexpr (EPI == VASR_EPI_GELU_PE) {
-                        v = gelu_erf(v) + auxb[(int64_t)row * p.ld_aux + col];
-                    }
-                    Cb[(int64_t)row * p.ldc + col] = v;
-                }
-            }
-        }
-    }
+    epilogue<TM, TN, EPI>(p, t, acc, wr, wc, r, h);
 }
 
 template <int WM, int WN, int TM, int TN>
@@ -253,77 +159,28 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     return launch_status("vasr_linear_f32");
 }
 
-// Tile configurations: {WM, WN, TM, TN, blocks per CU the kernel's VGPR/LDS use admits}.
-struct TileCfg {
-    int wm, wn, tm, tn, occ;
-    int bm() const { return wm * 32 * tm; }
-    int bn() const { return wn * 32 * tn; }
-};
 constexpr TileCfg kCfgs[] = {
     {2, 2, 2, 2, 3},  // 128 x 128
     {2, 2, 1, 2, 4},  //  64 x 128
     {4, 1, 1, 2, 4},  // 128 x  64
     {2, 2, 1, 1, 7},  //  64 x  64
 };
-constexpr int kCUs = 256;
-
-// Pick the tile that minimises (rounds of resident blocks) x (blocks sharing a CU) x tile area:
-// at M = 16032 the grids are only one or two rounds deep, so wave quantisation and CU
-// balance, not per-tile efficiency, decide the time (measured in tools/gemm_variants_run.py).
-int pick_cfg(int M, int N, int batch, bool pair) {
-    int best = -1;
-    double best_cost = 0;
-    for (int i = 0; i < 4; ++i) {
-        const TileCfg& c = kCfgs[i];
-        if (pair && c.tn != 2) continue;
-        const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
-        const long per_cu = (tiles + kCUs - 1) / kCUs;
-        const long rounds = (per_cu + c.occ - 1) / c.occ;
-        const double cost = (double)rounds * (double)(per_cu < c.occ ? per_cu : c.occ) * c.bm() * c.bn();
-        if (best < 0 || cost < best_cost * 0.999) {
-            best = i;
-            best_cost = cost;
-        }
-    }
-    return best;
-}
 
 }  // namespace
 }  // namespace vasr
 
 VASR_API int vasr_linear_f32(const vasr_gemm_args* a, void* stream) {
     using namespace vasr;
-    VASR_CHECK_ARG(a != nullptr, "vasr_linear_f32: null args");
-    VASR_CHECK_ARG(a->A && a->W && a->C, "vasr_linear_f32: null A/W/C");
-    VASR_CHECK_ARG(a->M >= 0 && a->N > 0 && a->K > 0 && a->batch >= 1, "vasr_linear_f32: bad shape M=%d N=%d K=%d batch=%d",
-                   a->M, a->N, a->K, a->batch);
-    VASR_CHECK_ARG(a->K % 4 == 0 && a->lda % 4 == 0 && a->ldw % 4 == 0 && a->stride_a % 4 == 0,
-                   "vasr_linear_f32: K, lda, ldw, stride_a must be multiples of 4 (K=%d lda=%lld)", a->K,
-                   (long long)a->lda);
-    VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->A) & 15) == 0 && (reinterpret_cast<uintptr_t>(a->W) & 15) == 0,
-                   "vasr_linear_f32: A and W must be 16-byte aligned");
+    GemmParams p;
+    if (int rc = check_args(a, "vasr_linear_f32", p)) return rc;
+    VASR_CHECK_ARG(a->W != nullptr, "vasr_linear_f32: null W");
+    VASR_CHECK_ARG(a->ldw % 4 == 0 && (reinterpret_cast<uintptr_t>(a->W) & 15) == 0,
+                   "vasr_linear_f32: W must be 16-byte aligned with ldw %% 4 == 0");
+    if (a->M == 0) return VASR_OK;
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
-    if (pair) {
-        VASR_CHECK_ARG(a->N % 64 == 0 && a->n_out > 0 && a->n_out <= a->N / 2,
-                       "vasr_linear_f32: paired epilogue needs N %% 64 == 0 and 0 < n_out <= N/2");
-    }
-    if (epi == VASR_EPI_RESIDUAL || epi == VASR_EPI_GELU_PE || epi == VASR_EPI_PAIR_FUSION)
-        VASR_CHECK_ARG(a->aux != nullptr, "vasr_linear_f32: epilogue %d needs aux", epi);
-    if (epi == VASR_EPI_PAIR_FUSION)
-        VASR_CHECK_ARG(a->aux2 != nullptr && a->bias != nullptr, "vasr_linear_f32: fusion needs bias and aux2");
-    if (a->M == 0) return VASR_OK;
-
-    GemmParams p;
-    p.A = a->A; p.lda = a->lda; p.stride_a = a->stride_a;
-    p.W = a->W; p.ldw = a->ldw; p.bias = a->bias;
-    p.C = a->C; p.ldc = a->ldc; p.stride_c = a->stride_c;
-    p.M = a->M; p.N = a->N; p.K = a->K;
-    p.aux = a->aux; p.ld_aux = a->ld_aux; p.stride_aux = a->stride_aux;
-    p.aux2 = a->aux2; p.n_out = a->n_out;
     hipStream_t s = as_stream(stream);
-
-    switch (pick_cfg(a->M, a->N, a->batch, pair)) {
+    switch (pick_cfg(kCfgs, 4, a->M, a->N, a->batch, pair)) {
         case 0: return launch_cfg<2, 2, 2, 2>(p, a->batch, epi, s);
         case 1: return launch_cfg<2, 2, 1, 2>(p, a->batch, epi, s);
         case 2: return launch_cfg<4, 1, 1, 2>(p, a->batch, epi, s);

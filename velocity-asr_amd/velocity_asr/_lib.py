@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libvasr_hip.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "vasr.h"))
@@ -45,6 +45,9 @@ _SIGNATURES = {
     "vasr_version": ([], ctypes.c_int),
     "vasr_last_error": ([], ctypes.c_char_p),
     "vasr_linear_f32": ([ctypes.POINTER(GemmArgs), c_p], ctypes.c_int),
+    "vasr_linear_x3_f32": ([ctypes.POINTER(GemmArgs), c_p, c_p], ctypes.c_int),
+    "vasr_split_weights_bf16x3": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
+    "vasr_split_weights_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_layer_norm_f32": ([c_p, c_i64, c_p, c_p, c_p, c_i64, ctypes.c_int, ctypes.c_int, c_f32, c_p], ctypes.c_int),
     "vasr_add_table_f32": ([c_p, c_p, c_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_p], ctypes.c_int),
     "vasr_ln_dwconv_f32": ([c_p, c_p, c_p, c_p, c_p, c_p] + [ctypes.c_int] * 4 + [c_f32, c_p], ctypes.c_int),

@@ -15,7 +15,6 @@ from __future__ import annotations
 
 import math
 import os
-import wave
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -34,25 +33,72 @@ N_MELS = 80
 WINDOW_FN = torch.hann_window
 
 
+_WAVE_PCM, _WAVE_FLOAT, _WAVE_EXTENSIBLE = 1, 3, 0xFFFE
+
+
 def _read_wav(path: str) -> Tuple[torch.Tensor, int]:
-    """PCM WAV reader (stdlib wave): (channels, samples) float32 in [-1, 1), like torchaudio.load."""
-    with wave.open(path, "rb") as w:
-        nch, width, sr, n = w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()
-        raw = w.readframes(n)
-    if width == 1:
-        x = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
+    """RIFF/WAVE reader: (channels, samples) float32, like torchaudio.load.
+
+    Integer PCM (8/16/24/32-bit) is scaled to [-1, 1); IEEE float (32/64-bit, format 3, or
+    WAVE_FORMAT_EXTENSIBLE with either sub-format) is returned as stored, so float32 clips
+    round-trip bit-exactly.
+    """
+    with open(path, "rb") as f:
+        data = f.read()
+    if len(data) < 12 or data[:4] != b"RIFF" or data[8:12] != b"WAVE":
+        raise ValueError(f"{path}: not a RIFF/WAVE file")
+    fmt = body = None
+    pos = 12
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], int.from_bytes(data[pos + 4:pos + 8], "little")
+        chunk = data[pos + 8:pos + 8 + size]
+        if cid == b"fmt ":
+            fmt = chunk
+        elif cid == b"data":
+            body = chunk
+        pos += 8 + size + (size & 1)
+    if fmt is None or body is None or len(fmt) < 16:
+        raise ValueError(f"{path}: missing fmt or data chunk")
+    tag, nch, sr = int.from_bytes(fmt[0:2], "little"), int.from_bytes(fmt[2:4], "little"), int.from_bytes(fmt[4:8], "little")
+    bits = int.from_bytes(fmt[14:16], "little")
+    if tag == _WAVE_EXTENSIBLE and len(fmt) >= 26:
+        tag = int.from_bytes(fmt[24:26], "little")
+    width = bits // 8
+    if nch < 1 or width < 1:
+        raise ValueError(f"{path}: bad format ({nch} channels, {bits} bits)")
+    body = body[: len(body) // (width * nch) * width * nch]
+    if tag == _WAVE_FLOAT and width in (4, 8):
+        x = np.frombuffer(body, "<f4" if width == 4 else "<f8").astype(np.float32)
+    elif tag != _WAVE_PCM:
+        raise ValueError(f"{path}: unsupported WAV format tag {tag}")
+    elif width == 1:
+        x = (np.frombuffer(body, np.uint8).astype(np.float32) - 128.0) / 128.0
     elif width == 2:
-        x = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
+        x = np.frombuffer(body, "<i2").astype(np.float32) / 32768.0
     elif width == 3:
-        b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
+        b = np.frombuffer(body, np.uint8).reshape(-1, 3).astype(np.int32)
         v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
         v = np.where(v >= 1 << 23, v - (1 << 24), v)
         x = v.astype(np.float32) / float(1 << 23)
     elif width == 4:
-        x = np.frombuffer(raw, "<i4").astype(np.float32) / float(1 << 31)
+        x = np.frombuffer(body, "<i4").astype(np.float32) / float(1 << 31)
     else:
-        raise ValueError(f"unsupported WAV sample width {width}")
+        raise ValueError(f"{path}: unsupported PCM sample width {width}")
     return torch.from_numpy(np.ascontiguousarray(x.reshape(-1, nch).T)), sr
+
+
+def write_wav(path: str, audio, sample_rate: int = SAMPLE_RATE) -> None:
+    """Write (samples,) or (channels, samples) audio as 32-bit IEEE-float WAV (lossless for float32)."""
+    x = np.asarray(audio.cpu().numpy() if isinstance(audio, torch.Tensor) else audio, dtype="<f4")
+    if x.ndim == 1:
+        x = x[None]
+    nch = x.shape[0]
+    body = np.ascontiguousarray(x.T).tobytes()
+    fmt = (_WAVE_FLOAT.to_bytes(2, "little") + nch.to_bytes(2, "little") + sample_rate.to_bytes(4, "little")
+           + (sample_rate * 4 * nch).to_bytes(4, "little") + (4 * nch).to_bytes(2, "little") + (32).to_bytes(2, "little"))
+    riff = b"WAVE" + b"fmt " + len(fmt).to_bytes(4, "little") + fmt + b"data" + len(body).to_bytes(4, "little") + body
+    with open(path, "wb") as f:
+        f.write(b"RIFF" + len(riff).to_bytes(4, "little") + riff)
 
 
 def load_audio(path: str, sample_rate: int = SAMPLE_RATE, mono: bool = True) -> torch.Tensor:

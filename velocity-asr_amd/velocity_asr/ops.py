@@ -8,6 +8,8 @@ and enqueues the kernel on the current HIP stream.  Nothing here computes on the
 from __future__ import annotations
 
 import math
+import os
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -78,6 +80,54 @@ def _rows(name: str, t: torch.Tensor) -> Tuple[int, int, int]:
     return t.shape[0], t.shape[1], t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
 
 
+# GEMM engine: "x3" = fp32 GEMM as split-bf16 products on the bf16 matrix cores
+# (vasr_linear_x3_f32, fp32-accurate, 2.67x the f32-MFMA rate); "f32" = f32-input MFMA.
+_GEMM_MODES = ("x3", "f32")
+_gemm_mode = os.environ.get("VASR_GEMM", "x3")
+if _gemm_mode not in _GEMM_MODES:
+    raise ValueError(f"VASR_GEMM={_gemm_mode!r}: expected one of {_GEMM_MODES}")
+
+
+def gemm_mode() -> str:
+    return _gemm_mode
+
+
+def set_gemm_mode(mode: str) -> str:
+    """Select the GEMM engine; returns the previous mode."""
+    global _gemm_mode
+    if mode not in _GEMM_MODES:
+        raise ValueError(f"gemm mode {mode!r}: expected one of {_GEMM_MODES}")
+    prev, _gemm_mode = _gemm_mode, mode
+    return prev
+
+
+# Split-bf16 planes of weight matrices, built once per (tensor, version) and dropped with the
+# tensor.  Keys are tensor identities: the model passes parameters or cached derived weights.
+_splits = {}
+
+
+def split_weights(w: torch.Tensor) -> torch.Tensor:
+    """[3][N][Kp] bf16 planes (as int16 storage) of a (N, K) fp32 weight view."""
+    N, K, ldw = _rows("split.w", w)
+    sig = (w.data_ptr(), w._version, N, K, ldw)
+    ent = _splits.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == sig:
+        return ent[2]
+    planes = torch.empty(int(L.lib().vasr_split_weights_elems(N, K)), device=w.device, dtype=torch.int16)
+    check(L.lib().vasr_split_weights_bf16x3(w.data_ptr(), ldw, N, K, planes.data_ptr(), stream_of(w)),
+          "vasr_split_weights_bf16x3")
+    key = id(w)
+    _splits[key] = (weakref.ref(w, lambda _r, k=key: _splits.pop(k, None)), sig, planes)
+    return planes
+
+
+def _linear(args: GemmArgs, w: torch.Tensor, stream) -> None:
+    if _gemm_mode == "x3":
+        check(L.lib().vasr_linear_x3_f32(args, split_weights(w).data_ptr(), stream), "vasr_linear_x3_f32")
+    else:
+        check(L.lib().vasr_linear_f32(args, stream), "vasr_linear_f32")
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, epilogue: int = L.EPI_NONE,
          out: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
          aux2: Optional[torch.Tensor] = None, n_out: int = 0, n_cols_out: Optional[int] = None) -> torch.Tensor:
@@ -105,7 +155,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     args.aux2 = ptr(aux2)
     args.n_out = n_out
     ev = _t0("gemm")
-    check(L.lib().vasr_linear_f32(args, stream_of(a)), "vasr_linear_f32")
+    _linear(args, w, stream_of(a))
     _t1("gemm", ev, dict(M=M, N=N, K=K, batch=1))
     return out
 
@@ -135,7 +185,7 @@ def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch
         args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, stride_aux
     args.n_out = n_out
     ev = _t0("gemm")
-    check(L.lib().vasr_linear_f32(args, stream_of(a_base)), "vasr_linear_f32")
+    _linear(args, w, stream_of(a_base))
     _t1("gemm", ev, dict(M=rows, N=N, K=K, batch=batch))
     return out
 

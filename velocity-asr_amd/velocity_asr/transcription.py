@@ -1,0 +1,147 @@
+"""File-level transcription used by scripts/transcribe.py and scripts/evaluate.py.
+
+The reference scripts run one file at a time: load -> mel on the host -> (1, F, 80) forward
+-> greedy decode (reference scripts/transcribe.py:48-131, scripts/evaluate.py:60-107).
+Here files are read on the host, then grouped by sample count and each group goes through
+the device pipeline as one batch (mel, forward, argmax, collapse all on the HIP device).
+Utterances are never padded — the model has no padding masks, so a padded clip would give
+different logits — and every utterance's computation is independent of its batch
+neighbours, so the output for a file is the one the per-file loop produces.
+"""
+
+from __future__ import annotations
+
+import logging
+from collections import OrderedDict
+from pathlib import Path
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+from .audio import HOP_LENGTH, SAMPLE_RATE, load_audio, mel_on_device
+from .decode import CTCDecoder, greedy_token_ids
+
+logger = logging.getLogger(__name__)
+
+AUDIO_EXTENSIONS = {".wav", ".mp3", ".flac", ".ogg", ".m4a"}
+
+
+def find_audio_files(directory: str) -> List[Path]:
+    """Recursive listing with the reference's extension set (scripts/transcribe.py:233-238)."""
+    return [p for p in Path(directory).rglob("*") if p.suffix.lower() in AUDIO_EXTENSIONS]
+
+
+def frames_to_seconds(frame_idx: int, hop_length: int = HOP_LENGTH, sample_rate: int = SAMPLE_RATE) -> float:
+    """Token frame -> seconds; tokens sit at stride 2 in mel frames (reference scripts/transcribe.py:42-45)."""
+    return (frame_idx * 2 * hop_length) / sample_rate
+
+
+def group_words(tokens: Sequence[int], spans: Sequence[Tuple[int, int]], vocabulary: Sequence[str]) -> List[Dict]:
+    """Word segmentation of a timed token list (reference scripts/transcribe.py:83-117).
+
+    A word is a run of non-separator characters (" " and "▁" separate). Its start is the
+    first character's start frame; its end is the end frame of the separator that closes
+    it, or of the utterance's last token for the final word — the reference's convention.
+    """
+    words: List[Dict] = []
+    chars: List[str] = []
+    first: Optional[int] = None
+
+    def flush(end_frame: int) -> None:
+        text = "".join(chars).replace("▁", "")
+        if text:
+            words.append({"word": text, "start": frames_to_seconds(first), "end": frames_to_seconds(end_frame)})
+
+    for tok, (s, e) in zip(tokens, spans):
+        ch = vocabulary[tok] if 0 <= tok < len(vocabulary) else "<unk>"
+        if ch in (" ", "▁"):
+            if chars:
+                flush(e)
+                chars, first = [], None
+        else:
+            if first is None:
+                first = s
+            chars.append(ch)
+    if chars and spans:
+        flush(spans[-1][1])
+    return words
+
+
+def _decode_batch(model, audio: torch.Tensor, decoder: CTCDecoder, timestamps: bool,
+                  beam_width: int = 1) -> List[Tuple[str, Optional[List[Dict]]]]:
+    """(b, S) device audio -> [(text, words or None)] through the device pipeline."""
+    with torch.no_grad():
+        mel = mel_on_device(audio, n_mels=model.config.mel_bins)
+        logits = model(mel)
+        if beam_width > 1:
+            return [(t, None) for t in decoder.decode_beam_search(logits, beam_width=beam_width)]
+        toks, lens, st, en = greedy_token_ids(logits, decoder.blank_token, True, timestamps)
+    toks, lens = toks.cpu().numpy(), lens.cpu().numpy()
+    if timestamps:
+        st, en = st.cpu().numpy(), en.cpu().numpy()
+    out = []
+    for b in range(toks.shape[0]):
+        n = int(lens[b])
+        ids = toks[b, :n].tolist()
+        if timestamps:
+            words = group_words(ids, list(zip(st[b, :n].tolist(), en[b, :n].tolist())), decoder.vocabulary)
+            out.append((" ".join(w["word"] for w in words), words))
+        else:
+            out.append((decoder._tokens_to_text(ids), None))
+    return out
+
+
+def transcribe_files(model, paths: Iterable, decoder: CTCDecoder, device, timestamps: bool = False,
+                     batch_size: int = 16, beam_width: int = 1) -> List[Dict]:
+    """Transcribe audio files; returns one result dict per file in input order.
+
+    A result is {"file", "duration", "transcription"} (+ "words" with timestamps), as the
+    reference's transcribe_file returns; a file that fails gets {"file", "error"} instead,
+    so callers can log it the way the reference's per-file try/except does.
+    """
+    paths = [str(p) for p in paths]
+    results: List[Optional[Dict]] = [None] * len(paths)
+    groups: "OrderedDict[int, List[Tuple[int, torch.Tensor]]]" = OrderedDict()
+    for i, p in enumerate(paths):
+        try:
+            a = load_audio(p)
+            if a.dim() != 1 or a.numel() < 2:
+                raise ValueError(f"expected a mono clip of at least 2 samples, got shape {tuple(a.shape)}")
+            groups.setdefault(a.numel(), []).append((i, a))
+        except Exception as e:  # reported per file, like the reference's loop
+            results[i] = {"file": p, "error": str(e)}
+    dev = torch.device(device)
+    for n, items in groups.items():
+        for k in range(0, len(items), max(1, batch_size)):
+            chunk = items[k:k + batch_size]
+            try:
+                audio = torch.stack([a for _, a in chunk]).to(dev, torch.float32)
+                decoded = _decode_batch(model, audio, decoder, timestamps, beam_width)
+                for (i, _), (text, words) in zip(chunk, decoded):
+                    r = {"file": paths[i], "duration": n / SAMPLE_RATE, "transcription": text}
+                    if timestamps:
+                        r["words"] = words
+                    results[i] = r
+            except Exception as e:
+                for i, _ in chunk:
+                    results[i] = {"file": paths[i], "error": str(e)}
+    return results  # type: ignore[return-value]
+
+
+def load_manifest(path: str) -> List[Tuple[str, str]]:
+    """Test-set manifest: one `audio_path<TAB>reference text` per line (relative paths are
+    resolved against the manifest's directory). The reference's load_test_data is a stub
+    that returns [] (scripts/evaluate.py:41-57); a manifest file is the local equivalent."""
+    p = Path(path)
+    if not p.is_file():
+        logger.warning(f"Dataset loading not implemented for '{path}'. Pass a TSV manifest file.")
+        return []
+    out = []
+    for line in p.read_text(encoding="utf-8").splitlines():
+        if not line.strip():
+            continue
+        audio, _, ref = line.partition("\t")
+        a = Path(audio)
+        out.append((str(a if a.is_absolute() else p.parent / a), ref))
+    return out
