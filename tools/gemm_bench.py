@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Time vasr_linear_f32 on the model's GEMM shapes (C2: B=32 x 10 s -> M = 16032 tokens)."""
+"""Time the GEMM engines (split-bf16 "x3" and f32-input MFMA) on the model's GEMM shapes
+(C2: B=32 x 10 s -> M = 16032 tokens).  Usage: gemm_bench.py [x3|f32 ...]"""
 import os
 import sys
 
@@ -21,6 +22,13 @@ SHAPES = [  # name, M, N, K, lda, epilogue, n_out
 
 
 def main():
+    for mode in (sys.argv[1:] or ["x3", "f32"]):
+        ops.set_gemm_mode(mode)
+        print(f"--- {mode}")
+        run()
+
+
+def run():
     reps = 30
     tot = 0.0
     for name, m, n, k, lda, epi, n_out in SHAPES:
@@ -41,8 +49,10 @@ def main():
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / reps * 1e3
         tf = 2 * m * n * k / us / 1e6
+        nbytes = 4 * (m * k + m * n * (2 if aux is not None else 1) + n * k)
         tot += us
-        print(f"{name:14s} M={m} N={n:4d} K={k}: {us:7.1f} us  {tf:6.1f} TFLOP/s ({tf / 157.3 * 100:4.1f}% of f32 peak)")
+        print(f"{name:14s} M={m} N={n:4d} K={k}: {us:7.1f} us  {tf:6.1f} TFLOP/s ({tf / 157.3 * 100:4.1f}% of f32 peak)"
+              f"  {nbytes / us / 1e3:6.0f} GB/s")
     print(f"sum {tot:.1f} us")
 
 

@@ -4,13 +4,14 @@
 set -e
 SRC=$1; VARIANTS=$2
 cd "$(dirname "$0")/../velocity-asr_amd"
-rm -rf ../tools/_variants && mkdir -p ../tools/_variants
+OUT=${OUT:-_variants}
+rm -rf ../tools/$OUT && mkdir -p ../tools/$OUT
 i=0
 for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include ${flags//,/ } \
-     -shared csrc/$SRC csrc/common.cpp -o ../tools/_variants/lib_${i}_${name}.so &
+     -shared csrc/$SRC csrc/common.cpp -o ../tools/$OUT/lib_${i}_${name}.so &
   i=$((i+1))
 done
 wait
-ls ../tools/_variants
+ls ../tools/$OUT

@@ -20,7 +20,7 @@ def main():
     A2 = -torch.arange(1, N + 1, device="cuda", dtype=torch.float32) * 1.4426950408889634
     D = torch.ones(Di, device="cuda")
     out = torch.empty(M, Di, device="cuda")
-    libs = sorted(glob.glob(os.path.join(HERE, "_variants", "lib_*.so")), key=lambda p: int(os.path.basename(p).split("_")[1]))
+    libs = sorted(glob.glob(os.path.join(HERE, os.environ.get("VARIANT_DIR", "_variants"), "lib_*.so")), key=lambda p: int(os.path.basename(p).split("_")[1]))
     fns = []
     for p in libs:
         lib = ctypes.CDLL(p)

@@ -31,6 +31,10 @@ using namespace gemm;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+#ifndef VASR_X3_ABLATE
+#define VASR_X3_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no C stores, 4 no A split,
+#endif                    // 8 no global loads after the first k-tile
+
 constexpr int BK = 32;      // fp32 k per LDS tile (two MFMA k-steps)
 constexpr int ROWB = 64;    // bytes per LDS row per plane (32 bf16)
 
@@ -107,7 +111,13 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
             const int row = q >> 3, c4 = q & 7;  // float4 c4 = half (c4 & 1) of chunk c4 >> 1
             const int off = swz(row, c4 >> 1) + 8 * (c4 & 1);
             bf16x4 hi, mid, lo;
-            split4(ra[i], hi, mid, lo);
+            if constexpr (VASR_X3_ABLATE & 4) {
+                hi = bf16x4{(__bf16)ra[i].x, (__bf16)ra[i].y, (__bf16)ra[i].z, (__bf16)ra[i].w};
+                mid = hi;
+                lo = hi;
+            } else {
+                split4(ra[i], hi, mid, lo);
+            }
             *reinterpret_cast<bf16x4*>(As + off) = hi;
             *reinterpret_cast<bf16x4*>(As + A_PLANE + off) = mid;
             *reinterpret_cast<bf16x4*>(As + 2 * A_PLANE + off) = lo;
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
     const int w_row = wc * 32 * TN + r;
 
     for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) load_tile((kt + 1) * BK);
+        if (kt + 1 < nk && !((VASR_X3_ABLATE & 8) && kt > 0)) load_tile((kt + 1) * BK);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int chunk = 2 * s + h;
@@ -152,6 +162,13 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
                     fw[pl][tn] = *reinterpret_cast<const bf16x8*>(Ws + pl * W_PLANE + swz(w_row + tn * 32, chunk));
             }
             // small terms first, then the leading hi*hi term
+            if constexpr (VASR_X3_ABLATE & 1) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)fa[0][tm][0] * (float)fw[2][tn][1];
+                continue;
+            }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -173,6 +190,16 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
         }
     }
 
+    if constexpr (VASR_X3_ABLATE & 2) {  // keep every accumulator live, store nothing
+        float sum = 0.f;
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sum += acc[tm][tn][i];
+        if (sum != 1.2345f) return;
+    }
     epilogue<TM, TN, EPI>(p, t, acc, wr, wc, r, h);
 }
 

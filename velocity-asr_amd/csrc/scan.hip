@@ -32,20 +32,34 @@
 namespace vasr {
 namespace {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 #ifndef VASR_SCAN_ABLATE
-#define VASR_SCAN_ABLATE 0  // diagnostic builds only (tools/scan_ablate.sh): 1 no exp, 2 no partial
-#endif                      // write, 4 no B/C LDS reads, 8 no chunk staging after the first
-#ifndef VASR_SCAN_DPP
-#define VASR_SCAN_DPP 1     // reduce the per-step partial sums across the G lanes with DPP
-#endif
+#define VASR_SCAN_ABLATE 0  // diagnostic builds only (tools/scan_ablate.sh): 1 no exp,
+#endif                      // 4 no B/C LDS reads, 8 no chunk staging after the first,
+                            // 16 no tree update, 32 no gated-output pass
 #ifndef VASR_SCAN_WAVES
 #define VASR_SCAN_WAVES 3   // waves per SIMD the register allocator targets
 #endif
+#ifndef VASR_SCAN_PACKED
+#define VASR_SCAN_PACKED 0  // 1: state pairs as float2 vectors (v_pk_*_f32)
+#endif
+
+// A pair of state values.  Packed v_pk_mul/add_f32 issue at half the rate of their scalar
+// forms on gfx950 (no throughput gain) and a dependent packed op needs a wait state, so the
+// default is a plain pair of scalars (the file is built with -fno-slp-vectorize).
+#if VASR_SCAN_PACKED
+typedef float f2 __attribute__((ext_vector_type(2)));
+#else
+struct f2 {
+    float x, y;
+};
+__device__ __forceinline__ f2 operator*(f2 a, f2 b) { return f2{a.x * b.x, a.y * b.y}; }
+__device__ __forceinline__ f2 operator+(f2 a, f2 b) { return f2{a.x + b.x, a.y + b.y}; }
+#endif
 
 constexpr int T = 16;    // time steps per chunk
+constexpr int TP = T + 1;  // padded row of the per-channel partial-sum tile
 constexpr int NPL = 4;   // state indices per lane (2 packed pairs)
 constexpr int NP = NPL / 2;
 constexpr int NW = 4;    // waves per block
@@ -74,6 +88,67 @@ __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
+constexpr int log2_c(int v) { return v <= 1 ? 0 : 1 + log2_c(v >> 1); }
+
+// Cross-lane reduction of 8 per-step partial sums over the G lanes of a channel, as a
+// transposing butterfly: each level halves the values a lane holds by exchanging the half it
+// gives away with its partner (DPP), so the 8 sums cost 7 exchanges and no wait states
+// (independent chains) instead of 8 dependent group_sum chains.  Partner masks xor 15, 7,
+// 2, 1 (row_mirror, row_half_mirror, quad_perm) keep partners in the same step subset.
+// Returns in v[0 .. S_f) the sums of steps j + S_f * (g >> (log2 G - nsplit)).
+template <int G>
+struct HalfReduce {
+    static constexpr int LG = log2_c(G);
+    static constexpr int NSPLIT = LG < 3 ? LG : 3;
+    static constexpr int SF = 8 >> NSPLIT;
+    static __device__ __forceinline__ int step(int j, int g) { return j + SF * (g >> (LG - NSPLIT)); }
+};
+
+template <int CTRL, int S>
+__device__ __forceinline__ void butterfly_level(float (&v)[8], bool sel) {
+    if constexpr (S >= 2) {
+#pragma unroll
+        for (int j = 0; j < S / 2; ++j) {
+            const float lo = v[j], hi = v[j + S / 2];
+            const float keep = sel ? hi : lo;
+            const float send = sel ? lo : hi;
+            v[j] = keep + dpp_mov<CTRL>(send);
+        }
+    } else {
+        v[0] = v[0] + dpp_mov<CTRL>(v[0]);
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void reduce_half(float (&v)[8], int g) {
+    if constexpr (G == 16) {
+        butterfly_level<0x140, 8>(v, (g >> 3) & 1);  // row_mirror: lane ^ 15
+        butterfly_level<0x141, 4>(v, (g >> 2) & 1);  // row_half_mirror: lane ^ 7
+        butterfly_level<0x4E, 2>(v, (g >> 1) & 1);   // quad_perm [2,3,0,1]: lane ^ 2
+        butterfly_level<0xB1, 1>(v, false);          // quad_perm [1,0,3,2]: lane ^ 1
+    } else if constexpr (G == 8) {
+        butterfly_level<0x141, 8>(v, (g >> 2) & 1);
+        butterfly_level<0x4E, 4>(v, (g >> 1) & 1);
+        butterfly_level<0xB1, 2>(v, g & 1);
+    } else {
+        static_assert(G == 4, "G in {4, 8, 16}");
+        butterfly_level<0x4E, 8>(v, (g >> 1) & 1);
+        butterfly_level<0xB1, 4>(v, g & 1);
+    }
+}
+
+// Reduce the partial sums of steps [8*HALF, 8*HALF + 8) and store them to the channel's row
+// of the partial-sum tile ([DPB][TP] floats).
+template <int G, int HALF>
+__device__ __forceinline__ void flush_half(float (&yv)[T], float* yp, int dl, int g) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = yv[HALF * 8 + j];
+    reduce_half<G>(v, g);
+#pragma unroll
+    for (int j = 0; j < HalfReduce<G>::SF; ++j) yp[dl * TP + HALF * 8 + HalfReduce<G>::step(j, g)] = v[j];
+}
+
 template <int MAXUP>
 struct TreeState {
     f2 la[4][NP], lb[4][NP], ca[4][NP], cb[4][NP];  // in-chunk levels 0..3
@@ -85,7 +160,7 @@ struct Smem {
     const float* xs;
     const float* dts;
     const float* bcs;
-    float* yp;  // partial sums [T][DPB][G]
+    float* yp;  // per-channel partial sums y[t] = sum_n h C: [DPB][TP]
 };
 
 // Per-step operands of one lane, read from the staged chunk one step ahead of use.
@@ -138,32 +213,39 @@ __device__ __forceinline__ StepElem make_elem(const StepIn& in, const f2 (&A2)[N
     return e;
 }
 
-// One push of the streaming tree scan at in-chunk step I; stores this lane's partial y.
+// One push of the streaming tree scan at in-chunk step I; leaves this lane's partial y in yv[I].
 template <int I, int MAXUP, int N, int DPB>
 __device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, const StepElem& el, int dl, int g,
-                                          f2 (&chunk_a)[NP], f2 (&chunk_b)[NP]) {
+                                          f2 (&chunk_a)[NP], f2 (&chunk_b)[NP], float (&yv)[T]) {
 #pragma clang fp contract(off)
     constexpr int G = N / NPL;
-    const f2 Cn[NP] = {{el.cv.x, el.cv.y}, {el.cv.z, el.cv.w}};
     // y contribution of h[t] (the exclusive prefix = cb of the current top block)
-    f2 part;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        f2 hv;
-        if constexpr (I == 0) hv = s.pb[p];
-        else hv = s.cb[ctz_c(I)][p];
-        part = p == 0 ? hv * Cn[p] : part + hv * Cn[p];
+    {
+        f2 h0, h1;
+        if constexpr (I == 0) {
+            h0 = s.pb[0];
+            h1 = s.pb[1];
+        } else {
+            h0 = s.cb[ctz_c(I)][0];
+            h1 = s.cb[ctz_c(I)][1];
+        }
+        float y = h0.x * el.cv.x;
+        y = __builtin_fmaf(h0.y, el.cv.y, y);
+        y = __builtin_fmaf(h1.x, el.cv.z, y);
+        yv[I] = __builtin_fmaf(h1.y, el.cv.w, y);
     }
-    if constexpr (VASR_SCAN_ABLATE & 2) {
-        if (part.x == 12345.f) sm.yp[(I * DPB + dl) * G + g] = part.y;
-    } else if constexpr (VASR_SCAN_DPP) {
-        const float y = group_sum<G>(part.x + part.y);
-        if (g == 0) sm.yp[I * DPB + dl] = y;
-    } else {
-        sm.yp[(I * DPB + dl) * G + g] = part.x + part.y;
-    }
+    if constexpr (I == 7) flush_half<G, 0>(yv, sm.yp, dl, g);
 
     constexpr int J = trailing_ones(I);
+    if constexpr (VASR_SCAN_ABLATE & 16) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            s.pb[p] = s.pb[p] + el.b[p];
+            s.pa[p] = el.a[p];
+        }
+        if constexpr (I == T - 1) flush_half<G, 1>(yv, sm.yp, dl, g);
+        return;
+    }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         f2 cur_a = el.a[p];
@@ -193,6 +275,7 @@ __device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, c
             chunk_b[p] = cur_b;
         }
     }
+    if constexpr (I == T - 1) flush_half<G, 1>(yv, sm.yp, dl, g);
 }
 
 template <int MAXUP>
@@ -240,25 +323,29 @@ template <int I, int MAXUP, int N, int DPB, bool FULL>
 struct TreeChunk {
     __device__ __forceinline__ static void run(TreeState<MAXUP>& s, const Smem& sm, const StepIn& raw_next,
                                                const StepElem& el, const f2 (&A2)[NP], int dl, int g, int nvalid,
-                                               f2 (&ca)[NP], f2 (&cb)[NP]) {
+                                               f2 (&ca)[NP], f2 (&cb)[NP], float (&yv)[T]) {
         if (FULL || I < nvalid) {
             StepIn raw2;
             if constexpr (I + 2 < T) raw2 = load_step<I + 2, N, DPB>(sm, dl, g);
             StepElem el_next;
             if constexpr (I + 1 < T) el_next = make_elem(raw_next, A2);
-            tree_step<I, MAXUP, N, DPB>(s, sm, el, dl, g, ca, cb);
-            TreeChunk<I + 1, MAXUP, N, DPB, FULL>::run(s, sm, raw2, el_next, A2, dl, g, nvalid, ca, cb);
+            tree_step<I, MAXUP, N, DPB>(s, sm, el, dl, g, ca, cb, yv);
+            TreeChunk<I + 1, MAXUP, N, DPB, FULL>::run(s, sm, raw2, el_next, A2, dl, g, nvalid, ca, cb, yv);
+        } else if constexpr (!FULL) {
+            // ragged last chunk: flush the partial sums of the steps that ran (the rest are 0)
+            if (I < 8) flush_half<N / NPL, 0>(yv, sm.yp, dl, g);
+            else flush_half<N / NPL, 1>(yv, sm.yp, dl, g);
         }
     }
 };
 template <int MAXUP, int N, int DPB, bool FULL>
 struct TreeChunk<T, MAXUP, N, DPB, FULL> {
     __device__ __forceinline__ static void run(TreeState<MAXUP>&, const Smem&, const StepIn&, const StepElem&,
-                                               const f2 (&)[NP], int, int, int, f2 (&)[NP], f2 (&)[NP]) {}
+                                               const f2 (&)[NP], int, int, int, f2 (&)[NP], f2 (&)[NP], float (&)[T]) {}
 };
 
 template <int N, int MODE, int MAXUP>
-__global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const float* __restrict__ xz, int64_t ld_xz,
+__global__ __launch_bounds__(256, MAXUP <= 5 ? VASR_SCAN_WAVES : 2) void ssm_scan_kernel(const float* __restrict__ xz, int64_t ld_xz,
                                                        const float* __restrict__ dt, int64_t ld_dt,
                                                        const float* __restrict__ bc, int64_t ld_bc,
                                                        const float* __restrict__ A2g, const float* __restrict__ Dg,
@@ -268,9 +355,9 @@ __global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const fl
     constexpr int G = N / NPL;       // lanes per channel
     constexpr int DPW = 64 / G;      // channels per wave
     constexpr int DPB = NW * DPW;    // channels per block
-    // LDS: two staging buffers {x, dt, z: T x DPB; bc: T x 2N}, partial sums T x DPB x G
+    // LDS: two staging buffers {x, dt, z: T x DPB; bc: T x 2N}, partial sums DPB x TP
     constexpr int BUF = 3 * T * DPB + T * 2 * N;
-    __shared__ __attribute__((aligned(16))) float smem[2 * BUF + T * DPB * (VASR_SCAN_DPP ? 1 : G)];
+    __shared__ __attribute__((aligned(16))) float smem[2 * BUF + DPB * TP];
     float* ypart = smem + 2 * BUF;
 
     // XCD-aware block mapping: blocks id, id+8, id+16, ... share an XCD; give each such
@@ -345,13 +432,17 @@ __global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const fl
 
         if constexpr (MODE == 0) {
             f2 cha[NP], chb[NP];
+            float yv[T];
             const StepIn r0 = load_step<0, N, DPB>(sm, dl, g);
             const StepIn r1 = load_step<1, N, DPB>(sm, dl, g);
             const StepElem e0 = make_elem(r0, A2);
-            if (nvalid == T)
-                TreeChunk<0, MAXUP, N, DPB, true>::run(st, sm, r1, e0, A2, dl, g, nvalid, cha, chb);
-            else
-                TreeChunk<0, MAXUP, N, DPB, false>::run(st, sm, r1, e0, A2, dl, g, nvalid, cha, chb);
+            if (nvalid == T) {
+                TreeChunk<0, MAXUP, N, DPB, true>::run(st, sm, r1, e0, A2, dl, g, nvalid, cha, chb, yv);
+            } else {
+#pragma unroll
+                for (int j = 0; j < T; ++j) yv[j] = 0.0f;
+                TreeChunk<0, MAXUP, N, DPB, false>::run(st, sm, r1, e0, A2, dl, g, nvalid, cha, chb, yv);
+            }
             if (c + 1 < nchunks) merge_upper<MAXUP>(st, cha, chb, c);
         } else {
             for (int i = 0; i < nvalid; ++i) {
@@ -370,12 +461,8 @@ __global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const fl
                     h[p] = dA * h[p] + xv2 * dB;
                     part = part + h[p] * Cn[p];
                 }
-                if constexpr (VASR_SCAN_DPP) {
-                    const float y = group_sum<G>(part.x + part.y);
-                    if (g == 0) ypart[i * DPB + dl] = y;
-                } else {
-                    ypart[(i * DPB + dl) * G + g] = part.x + part.y;
-                }
+                const float y = group_sum<G>(part.x + part.y);
+                if (g == 0) ypart[dl * TP + i] = y;
             }
         }
         __syncthreads();
@@ -383,19 +470,8 @@ __global__ __launch_bounds__(256, VASR_SCAN_WAVES) void ssm_scan_kernel(const fl
         for (int idx = tid; idx < T * DPB; idx += 64 * NW) {
             const int t = idx / DPB, d = idx - t * DPB;
             if (t < nvalid) {
-                float ysum;
-                if constexpr (VASR_SCAN_DPP) {
-                    ysum = ypart[t * DPB + d];
-                } else {
-                    const float4* pp = reinterpret_cast<const float4*>(ypart + (t * DPB + d) * G);
-                    float4 acc = pp[0];
-#pragma unroll
-                    for (int k = 1; k < G / 4; ++k) {
-                        const float4 v = pp[k];
-                        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-                    }
-                    ysum = (acc.x + acc.y) + (acc.z + acc.w);
-                }
+                const float ysum = ypart[d * TP + t];
+                if ((VASR_SCAN_ABLATE & 32) && ysum != 1.2345f) continue;
                 const float xv = sm.xs[t * DPB + d];
                 const float zv = zs[t * DPB + d];
                 const float y = ysum + xv * Dd;
