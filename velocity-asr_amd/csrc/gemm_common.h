@@ -65,22 +65,31 @@ __device__ __forceinline__ Tile decode_tile(const GemmParams& p) {
 // two views of the same 32 output columns in the same lane and register: PAIR_POWER puts
 // DFT cos|sin rows side by side (|X|^2 in-register); PAIR_FUSION puts the gate and
 // global_proj rows side by side (gated fusion in-register).
-template <int TM, int TN, int EPI>
-__device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, floatx16 (&acc)[TM][TN], int wr,
-                                         int wc, int r, int h) {
+//
+// GUARD = false for tiles wholly inside M x N: no per-element bounds branches.
+template <int TM, int TN, int EPI, bool GUARD>
+__device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t, floatx16 (&acc)[TM][TN], int wr,
+                                              int wc, int r, int h) {
     float* __restrict__ Cb = p.C + (int64_t)t.bz * p.stride_c;
     const float* __restrict__ auxb = p.aux ? p.aux + (int64_t)t.bz * p.stride_aux : nullptr;
     const int m0 = t.m0, n0 = t.n0;
 
     if constexpr (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) {
         const int col = (n0 + wc * 32 * TN) / 2 + r;  // output column of this lane
-        if (col >= p.n_out) return;
+        if (GUARD && col >= p.n_out) return;
+        float bg = 0.f, bgl = 0.f, b2 = 0.f;
+        const int pc = n0 + wc * 32 * TN + r;  // paired column of half 0
+        if constexpr (EPI == VASR_EPI_PAIR_FUSION) {
+            bg = p.bias[pc];
+            bgl = p.bias[pc + 32];
+            b2 = p.aux2[col];
+        }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (row >= p.M) continue;
+                if (GUARD && row >= p.M) continue;
                 const float v0 = acc[tm][0][i];
                 const float v1 = acc[tm][TN - 1][i];
                 float out;
@@ -88,11 +97,10 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, flo
                     out = v0 * v0 + v1 * v1;
                 } else {
                     // aux: local-side partial products in the same paired layout.
-                    const int pc = n0 + wc * 32 * TN + r;  // paired column of half 0
                     const float* ar = auxb + (int64_t)row * p.ld_aux;
-                    const float gate = sigmoidf_((ar[pc] + v0) + p.bias[pc]);
-                    const float lt = ar[pc + 32] + p.aux2[col];
-                    const float gt = v1 + p.bias[pc + 32];
+                    const float gate = sigmoid_fast((ar[pc] + v0) + bg);
+                    const float lt = ar[pc + 32] + b2;
+                    const float gt = v1 + bgl;
                     out = gate * lt + (1.0f - gate) * gt;
                 }
                 Cb[(int64_t)row * p.ldc + col] = out;
@@ -104,28 +112,43 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, flo
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn) {
                 const int col = n0 + wc * 32 * TN + tn * 32 + r;
-                if (col >= p.N) continue;
+                if (GUARD && col >= p.N) continue;
                 const float bv = p.bias ? p.bias[col] : 0.0f;
+                // softplus columns: decided per 32-column MFMA tile (wave-uniform) where possible
+                const int cbase = n0 + wc * 32 * TN + tn * 32;
+                const bool sp_all = cbase >= p.n_out, sp_none = cbase + 32 <= p.n_out;
+                const bool sp = col >= p.n_out;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    if (row >= p.M) continue;
+                    if (GUARD && row >= p.M) continue;
                     float v = acc[tm][tn][i];
                     if (p.bias) v = v + bv;
                     if constexpr (EPI == VASR_EPI_GELU) {
-                        v = gelu_erf(v);
+                        v = gelu_fast(v);
                     } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
-                        if (col >= p.n_out) v = softplus20(v);
+                        if (sp_all) v = softplus20_fast(v);
+                        else if (!sp_none) v = sp ? softplus20_fast(v) : v;
                     } else if constexpr (EPI == VASR_EPI_RESIDUAL) {
                         v = v + auxb[(int64_t)row * p.ld_aux + col];
                     } else if constexpr (EPI == VASR_EPI_GELU_PE) {
-                        v = gelu_erf(v) + auxb[(int64_t)row * p.ld_aux + col];
+                        v = gelu_fast(v) + auxb[(int64_t)row * p.ld_aux + col];
                     }
                     Cb[(int64_t)row * p.ldc + col] = v;
                 }
             }
         }
     }
+}
+
+template <int BM, int BN, int TM, int TN, int EPI>
+__device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, floatx16 (&acc)[TM][TN], int wr,
+                                         int wc, int r, int h) {
+    const int ncols = (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) ? 2 * p.n_out : p.N;
+    if (t.m0 + BM <= p.M && t.n0 + BN <= ncols)
+        epilogue_body<TM, TN, EPI, false>(p, t, acc, wr, wc, r, h);
+    else
+        epilogue_body<TM, TN, EPI, true>(p, t, acc, wr, wc, r, h);
 }
 
 // Tile configurations: {WM, WN, TM, TN, blocks per CU the kernel's VGPR/LDS use admits}.

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
         }
     }
 
-    epilogue<TM, TN, EPI>(p, t, acc, wr, wc, r, h);
+    epilogue<BM, BN, TM, TN, EPI>(p, t, acc, wr, wc, r, h);
 }
 
 template <int WM, int WN, int TM, int TN>

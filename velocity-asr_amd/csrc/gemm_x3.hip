@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
                 for (int i = 0; i < 16; ++i) sum += acc[tm][tn][i];
         if (sum != 1.2345f) return;
     }
-    epilogue<TM, TN, EPI>(p, t, acc, wr, wc, r, h);
+    epilogue<BM, BN, TM, TN, EPI>(p, t, acc, wr, wc, r, h);
 }
 
 template <int WM, int WN, int TM, int TN>

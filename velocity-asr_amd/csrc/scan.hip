@@ -42,12 +42,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define VASR_SCAN_WAVES 3   // waves per SIMD the register allocator targets
 #endif
 #ifndef VASR_SCAN_PACKED
-#define VASR_SCAN_PACKED 0  // 1: state pairs as float2 vectors (v_pk_*_f32)
+#define VASR_SCAN_PACKED 1  // 1: state pairs as float2 vectors (v_pk_*_f32); 0: scalar pairs
 #endif
 
 // A pair of state values.  Packed v_pk_mul/add_f32 issue at half the rate of their scalar
-// forms on gfx950 (no throughput gain) and a dependent packed op needs a wait state, so the
-// default is a plain pair of scalars (the file is built with -fno-slp-vectorize).
+// forms on gfx950 (no FLOP gain) but halve the instruction count; measured 4 % faster than
+// scalar pairs here (tools/scan_ablate.sh), so packed is the default.
 #if VASR_SCAN_PACKED
 typedef float f2 __attribute__((ext_vector_type(2)));
 #else
@@ -278,41 +278,63 @@ __device__ __forceinline__ void tree_step(TreeState<MAXUP>& s, const Smem& sm, c
     if constexpr (I == T - 1) flush_half<G, 1>(yv, sm.yp, dl, g);
 }
 
-template <int MAXUP>
-__device__ __forceinline__ void merge_upper(TreeState<MAXUP>& s, const f2 (&chunk_a)[NP], const f2 (&chunk_b)[NP],
-                                            int cc) {
+// Merge the finished chunk block into the upper (chunk-level) stack when the chunk counter
+// cc has J trailing ones (J = levels to merge, a wave-uniform value: one switch case runs),
+// then rebuild the prefix after the upper stack bottom-up from the stream form's (1, 0)
+// start: the same float operations as carrying (ca, cb) per upper entry.  The levels set in
+// cc + 1 are J and those above J that were set in cc; the uniform per-level tests branch.
+template <int J, int MAXUP>
+__device__ __forceinline__ void merge_upper_j(TreeState<MAXUP>& s, const f2 (&chunk_a)[NP], const f2 (&chunk_b)[NP],
+                                              int cc1) {
 #pragma clang fp contract(off)
-    const int j = __builtin_ctz(~cc);
-    const int cc1 = cc + 1;
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         f2 cur_a = chunk_a[p], cur_b = chunk_b[p];
 #pragma unroll
-        for (int u = 0; u < MAXUP; ++u) {
-            if (u < j) {
-                cur_b = cur_a * s.ulb[u][p] + cur_b;
-                cur_a = cur_a * s.ula[u][p];
-            }
+        for (int u = 0; u < J; ++u) {
+            cur_b = cur_a * s.ulb[u][p] + cur_b;
+            cur_a = cur_a * s.ula[u][p];
         }
+        s.ula[J][p] = cur_a;
+        s.ulb[J][p] = cur_b;
+    }
+    f2 pa[NP], pb[NP];
 #pragma unroll
-        for (int u = 0; u < MAXUP; ++u) {
-            if (u == j) {
-                s.ula[u][p] = cur_a;
-                s.ulb[u][p] = cur_b;
-            }
-        }
-        // Prefix after the upper stack, rebuilt bottom-up from the stream form's (1, 0) start:
-        // the same float operations as carrying (ca, cb) per upper entry.
-        f2 pa = {1.0f, 1.0f}, pb = {0.0f, 0.0f};
+    for (int p = 0; p < NP; ++p) {
+        pa[p] = f2{1.0f, 1.0f};
+        pb[p] = f2{0.0f, 0.0f};
+    }
 #pragma unroll
-        for (int u = MAXUP - 1; u >= 0; --u) {
-            if ((cc1 >> u) & 1) {
-                pa = pa * s.ula[u][p];
-                pb = pa * s.ulb[u][p] + pb;
+    for (int u = MAXUP - 1; u > J; --u) {
+        if ((cc1 >> u) & 1) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                pa[p] = pa[p] * s.ula[u][p];
+                pb[p] = pa[p] * s.ulb[u][p] + pb[p];
             }
         }
-        s.pa[p] = pa;
-        s.pb[p] = pb;
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        s.pa[p] = pa[p] * s.ula[J][p];
+        s.pb[p] = s.pa[p] * s.ulb[J][p] + pb[p];
+    }
+}
+
+template <int MAXUP>
+__device__ __forceinline__ void merge_upper(TreeState<MAXUP>& s, const f2 (&chunk_a)[NP], const f2 (&chunk_b)[NP],
+                                            int cc) {
+    const int cc1 = cc + 1;
+    switch (__builtin_ctz(~cc)) {
+        case 0: merge_upper_j<0, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 1: if constexpr (MAXUP > 1) merge_upper_j<1, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 2: if constexpr (MAXUP > 2) merge_upper_j<2, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 3: if constexpr (MAXUP > 3) merge_upper_j<3, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 4: if constexpr (MAXUP > 4) merge_upper_j<4, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 5: if constexpr (MAXUP > 5) merge_upper_j<5, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 6: if constexpr (MAXUP > 6) merge_upper_j<6, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        case 7: if constexpr (MAXUP > 7) merge_upper_j<7, MAXUP>(s, chunk_a, chunk_b, cc1); break;
+        default: if constexpr (MAXUP > 8) merge_upper_j<8, MAXUP>(s, chunk_a, chunk_b, cc1); break;
     }
 }
 
@@ -355,10 +377,14 @@ __global__ __launch_bounds__(256, MAXUP <= 5 ? VASR_SCAN_WAVES : 2) void ssm_sca
     constexpr int G = N / NPL;       // lanes per channel
     constexpr int DPW = 64 / G;      // channels per wave
     constexpr int DPB = NW * DPW;    // channels per block
-    // LDS: two staging buffers {x, dt, z: T x DPB; bc: T x 2N}, partial sums DPB x TP
+    // LDS: two staging buffers {x, dt, z: T x DPB; bc: T x 2N}, partial sums DPB x TP.  The
+    // buffers are distinct objects and the chunk loop is unrolled by two, so the compiler can
+    // tell that reads of one buffer do not alias the LDS-DMA into the other and does not drain
+    // the prefetch (vmcnt(0)) before them.
     constexpr int BUF = 3 * T * DPB + T * 2 * N;
-    __shared__ __attribute__((aligned(16))) float smem[2 * BUF + DPB * TP];
-    float* ypart = smem + 2 * BUF;
+    __shared__ __attribute__((aligned(16))) float sbuf0[BUF];
+    __shared__ __attribute__((aligned(16))) float sbuf1[BUF];
+    __shared__ __attribute__((aligned(16))) float ypart[DPB * TP];
 
     // XCD-aware block mapping: blocks id, id+8, id+16, ... share an XCD; give each such
     // group consecutive (b, channel-block) work items so one utterance stays on one L2.
@@ -409,7 +435,7 @@ __global__ __launch_bounds__(256, MAXUP <= 5 ? VASR_SCAN_WAVES : 2) void ssm_sca
     };
 
     const int nchunks = (L + T - 1) / T;
-    load_chunk(0, smem);
+    load_chunk(0, sbuf0);
     __syncthreads();
     const float Dd = Dg[d0 + tid % DPB];
 
@@ -422,13 +448,12 @@ __global__ __launch_bounds__(256, MAXUP <= 5 ? VASR_SCAN_WAVES : 2) void ssm_sca
         h[p] = f2{0.0f, 0.0f};
     }
 
-    for (int c = 0; c < nchunks; ++c) {
-        float* buf = smem + (c & 1) * BUF;
+    auto chunk = [&](int c, float* buf, float* nbuf) {
         Smem sm{buf, buf + T * DPB, buf + 3 * T * DPB, ypart};
         const float* zs = buf + 2 * T * DPB;
         const int t0 = c * T;
         const int nvalid = min(T, L - t0);
-        if (c + 1 < nchunks && !((VASR_SCAN_ABLATE & 8) && c > 0)) load_chunk(t0 + T, smem + ((c + 1) & 1) * BUF);
+        if (c + 1 < nchunks && !((VASR_SCAN_ABLATE & 8) && c > 0)) load_chunk(t0 + T, nbuf);
 
         if constexpr (MODE == 0) {
             f2 cha[NP], chb[NP];
@@ -465,7 +490,9 @@ __global__ __launch_bounds__(256, MAXUP <= 5 ? VASR_SCAN_WAVES : 2) void ssm_sca
                 if (g == 0) ypart[dl * TP + i] = y;
             }
         }
-        __syncthreads();
+        // partial sums visible to all waves; the LDS-DMA of chunk c+1 stays in flight
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+        __builtin_amdgcn_s_barrier();
         // gated output of this chunk: (sum_g partials + x D) * silu(z), coalesced along d
         for (int idx = tid; idx < T * DPB; idx += 64 * NW) {
             const int t = idx / DPB, d = idx - t * DPB;
@@ -480,6 +507,10 @@ __global__ __launch_bounds__(256, MAXUP <= 5 ? VASR_SCAN_WAVES : 2) void ssm_sca
             }
         }
         __syncthreads();  // also drains this wave's LDS-DMA of chunk c+1 (vmcnt(0) before the barrier)
+    };
+    for (int c = 0; c < nchunks; c += 2) {
+        chunk(c, sbuf0, sbuf1);
+        if (c + 1 < nchunks) chunk(c + 1, sbuf1, sbuf0);
     }
 }
 

@@ -54,6 +54,37 @@ __device__ __forceinline__ float softplus20(float x) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Epilogue forms on the hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp
+// each): 12-20 instructions instead of the 55-130 of the libm forms above, which dominated
+// the GEMM epilogues.  Accuracy is stated per function; the parity tests bound the effect.
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
+// erfc(a) for a >= 0 as q(t) exp(-a^2), t = 1 / (1 + p a) (Abramowitz & Stegun 7.1.26,
+// |error of erf| <= 1.5e-7); GELU(x) = x (1 - q/2) for x >= 0 and x q/2 below, which keeps
+// the small negative tail relatively accurate.
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float a = fabsf(x) * 0.70710678118654752440f;
+    const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, a, 1.0f));
+    float q = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+    q = __builtin_fmaf(q, t, 1.421413741f);
+    q = __builtin_fmaf(q, t, -0.284496736f);
+    q = __builtin_fmaf(q, t, 0.254829592f);
+    q = q * t * fast_exp(-a * a);
+    return x >= 0.0f ? x * __builtin_fmaf(-0.5f, q, 1.0f) : 0.5f * x * q;
+}
+
+// softplus(x) = max(x, 0) + log1p(exp(-|x|)); log1p(e) = log(u) * e / (u - 1) with u = 1 + e
+// (compensates the rounding of u), e itself when u rounds to 1.  Threshold 20 as torch.
+__device__ __forceinline__ float softplus20_fast(float x) {
+    const float e = fast_exp(-fabsf(x));
+    const float u = 1.0f + e;
+    const float d = u - 1.0f;
+    const float l = d == 0.0f ? e : __builtin_amdgcn_logf(u) * 0.69314718055994531f * (e * __builtin_amdgcn_rcpf(d));
+    return x > 20.0f ? x : fmaxf(x, 0.0f) + l;
+}
+
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + fast_exp(-x)); }
+
 }  // namespace vasr
 
 #define VASR_CHECK_ARG(cond, ...)            \
