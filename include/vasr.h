@@ -88,8 +88,10 @@ int vasr_linear_f32(const vasr_gemm_args* args, void* stream);
  */
 int vasr_linear_x3_f32(const vasr_gemm_args* args, const uint16_t* w_split, void* stream);
 
-/* Split W (N x K fp32, row stride ldw) into bf16 planes out[3][N][Kp] (hi, mid, lo;
- * Kp = K rounded up to 32, zero padded).  vasr_split_weights_elems(N, K) = 3*N*Kp. */
+/* Split W (N x K fp32, row stride ldw) into bf16 terms (hi, mid, lo) in the fragment-native
+ * layout out[NT][KS][3][64][8] (NT = ceil(N/32), KS = Kp/16, Kp = K rounded up to 32):
+ * element (n, k) of plane p is out[n/32][k/16][p][32*((k%16)/8) + n%32][k%8]; padding is
+ * zero.  vasr_split_weights_elems(N, K) = 3 * 32*NT * Kp. */
 int vasr_split_weights_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
 int64_t vasr_split_weights_elems(int N, int K);
 

@@ -135,15 +135,19 @@ def test_gemm_x3_accuracy_matches_f32(va):
 
 
 def test_split_weights_planes(va):
-    """hi + mid + lo reproduces every fp32 weight exactly; K padded with zeros."""
+    """hi + mid + lo reproduces every fp32 weight exactly in the fragment-native layout
+    [N/32][Kp/16][3][64][8]; rows >= N and k >= K are zero."""
     from velocity_asr import ops
     g = torch.Generator().manual_seed(5)
-    w = (torch.randn(70, 100, generator=g) * torch.exp2(torch.randint(-30, 31, (70, 100), generator=g).float()))
-    planes = ops.split_weights(w.to(DEV)).cpu().view(3, 70, 128)
-    f = (planes.to(torch.int32) & 0xFFFF) << 16
-    vals = f.view(torch.float32).double()
-    np.testing.assert_array_equal(vals.sum(0)[:, :100].float().numpy(), w.numpy())
-    assert (planes[:, :, 100:] == 0).all()
+    N, K = 70, 100
+    w = (torch.randn(N, K, generator=g) * torch.exp2(torch.randint(-30, 31, (N, K), generator=g).float()))
+    NT, KS = 3, 8
+    planes = ops.split_weights(w.to(DEV)).cpu().view(NT, KS, 3, 2, 32, 8)  # [nt][ks][pl][h][r][j]
+    f = ((planes.to(torch.int32) & 0xFFFF) << 16).view(torch.float32).double()
+    # (nt, r) -> n ; (ks, h, j) -> k
+    dense = f.permute(2, 0, 4, 1, 3, 5).reshape(3, NT * 32, KS * 16)
+    np.testing.assert_array_equal(dense.sum(0)[:N, :K].float().numpy(), w.numpy())
+    assert (dense[:, N:, :] == 0).all() and (dense[:, :, K:] == 0).all()
 
 
 def test_layer_norm_and_dwconv(va):

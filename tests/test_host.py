@@ -39,7 +39,7 @@ def test_abi_rejects_bad_arguments_without_gpu():
     assert L.vasr_linear_f32(ctypes.byref(args), None) == -1
     assert L.vasr_linear_x3_f32(ctypes.byref(args), None, None) == -1
     assert L.vasr_split_weights_bf16x3(None, 4, 4, 4, None, None) == -1
-    assert L.vasr_split_weights_elems(70, 100) == 3 * 70 * 128
+    assert L.vasr_split_weights_elems(70, 100) == 3 * 96 * 128
 
 
 def test_public_api_matches_reference_all():

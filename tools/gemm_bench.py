@@ -29,9 +29,12 @@ def main():
 
 
 def run():
-    reps = 30
+    reps = int(os.environ.get("GEMM_REPS", "30"))
+    only = os.environ.get("GEMM_SHAPES")
     tot = 0.0
     for name, m, n, k, lda, epi, n_out in SHAPES:
+        if only and name not in only.split(","):
+            continue
         a = torch.randn(m, lda, device="cuda")[:, :k]
         w = torch.randn(n, k, device="cuda") * 0.05
         b = torch.randn(n, device="cuda")

@@ -11,16 +11,23 @@
 // MFMAs (32 cycles each per 32x32x16) replace eight f32 MFMAs (64 cycles per 32x32x2) per
 // 16 k-steps: 2.67x the f32-input MFMA rate (MI355X_MICROARCH.md, cycle constants).
 //
-// Weights are split once (vasr_split_weights_bf16x3) into planes [3][N][Kp] bf16.  The
-// activation tile is split on its way into LDS.  LDS holds, per k-tile of 32, three planes
-// for A (BM rows) and three for W (BN rows), 64 B per row, 16-B chunk c of row r stored at
-// chunk c ^ ((r >> 2) & 3): every ds_read_b128 lane group of the operand reads (lanes
-// r = 0..31 of one row block, one chunk) then hits 16 distinct 16-B slots of the 256-B bank
-// row (conflict-free; MI355X_MICROARCH.md §LDS lane groups).
+// Staging: both operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// wave-instruction, no VGPRs) into two double-buffer sets that are distinct LDS objects (the
+// k loop is unrolled by two), so the compiler does not drain the in-flight prefetch before the
+// current buffer's reads; one barrier per k-tile of 32.
+//  * A stays fp32 in LDS, [BM][32] with 16-B chunk c of row r at position c ^ f(r),
+//    f(r) = ((r >> 1) & 3) ^ (((r >> 3) & 1) << 2): every ds_read_b128 lane group of the
+//    fragment read (16 rows, one chunk) then hits 16 distinct 16-B slots of the 256-B bank row
+//    (MI355X_MICROARCH.md §LDS lane groups).  LDS-DMA writes lane-linearly, so the swizzle is
+//    applied to the source address.  Each wave splits its fragments after the read (VALU that
+//    runs in the MFMA shadow).
+//  * W is split once (vasr_split_weights_bf16x3) into a fragment-native layout
+//    [N/32][Kp/16][3 planes][64 lanes][8 bf16]: one k-step of one plane of one 32-column tile
+//    is 1 KiB in lane order, so LDS-DMA and the ds_read_b128 fragment reads are both linear.
 //
 // Operand maps (cdna_hip_programming.md §3): lane (r = lane & 31, h = lane >> 5) supplies
-// A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7, i.e. chunk 2s + h of k-step s.
-// The accumulator layout equals the f32-input MFMA's, so gemm_common.h's epilogues apply.
+// A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7.  The accumulator layout equals the
+// f32-input MFMA's, so gemm_common.h's epilogues apply.
 #include "gemm_common.h"
 
 namespace vasr {
@@ -29,44 +36,51 @@ namespace {
 using namespace gemm;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 #ifndef VASR_X3_ABLATE
-#define VASR_X3_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no C stores, 4 no A split,
-#endif                    // 8 no global loads after the first k-tile
+#define VASR_X3_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no C stores
+#endif
 
-constexpr int BK = 32;      // fp32 k per LDS tile (two MFMA k-steps)
-constexpr int ROWB = 64;    // bytes per LDS row per plane (32 bf16)
+typedef __attribute__((address_space(3))) void lds_void;
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * ROWB + 16 * (chunk ^ ((row >> 2) & 3)); }
+constexpr int BK = 32;  // fp32 k per stage (two MFMA k-steps)
 
-__device__ __forceinline__ void split4(const float4& x, bf16x4& hi, bf16x4& mid, bf16x4& lo) {
-    const float v[4] = {x.x, x.y, x.z, x.w};
+__device__ __forceinline__ int a_swz(int r) { return ((r >> 1) & 3) ^ (((r >> 3) & 1) << 2); }
+
+__device__ __forceinline__ void split1(float v, __bf16& hi, __bf16& mid, __bf16& lo) {
+    hi = (__bf16)v;
+    const float r1 = v - (float)hi;
+    mid = (__bf16)r1;
+    lo = (__bf16)(r1 - (float)mid);
+}
+
+__device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const __bf16 a = (__bf16)v[j];
-        const float r1 = v[j] - (float)a;
-        const __bf16 b = (__bf16)r1;
-        const float r2 = r1 - (float)b;
+    for (int j = 0; j < 8; ++j) {
+        __bf16 a, b, c;
+        split1(v[j], a, b, c);
         hi[j] = a;
         mid[j] = b;
-        lo[j] = (__bf16)r2;
+        lo[j] = c;
     }
 }
 
 template <int WM, int WN, int TM, int TN, int EPI>
-__global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
+__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
+    static_assert(WM * WN == 4, "4 waves");
     static_assert(TN == 2 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need TN=2");
-    constexpr int A_LOADS = BM * (BK / 4) / 256;      // float4 of A per thread per tile
-    constexpr int W_LOADS = 3 * BN * (BK / 8) / 256;  // 16-B bf16 chunks of W per thread per tile
-    static_assert(A_LOADS >= 1 && W_LOADS >= 1 && (3 * BN * 4) % 256 == 0, "tile too small");
-    constexpr int A_PLANE = BM * ROWB, W_PLANE = BN * ROWB;
+    constexpr int A_BYTES = BM * BK * 4;            // fp32 [BM][32]
+    constexpr int W_BYTES = (BN / 32) * 6 * 1024;   // [BN/32][2 k-steps][3 planes][64][16 B]
+    constexpr int A_INSTR = A_BYTES / 1024, W_INSTR = W_BYTES / 1024;
+    static_assert(A_INSTR % 4 == 0 && W_INSTR % 4 == 0, "whole LDS-DMA pieces per wave");
 
-    __shared__ __attribute__((aligned(16))) char smem[3 * (A_PLANE + W_PLANE)];
-    char* As = smem;
-    char* Ws = smem + 3 * A_PLANE;
+    __shared__ __attribute__((aligned(16))) char a0[A_BYTES];
+    __shared__ __attribute__((aligned(16))) char w0[W_BYTES];
+    __shared__ __attribute__((aligned(16))) char a1[A_BYTES];
+    __shared__ __attribute__((aligned(16))) char w1[W_BYTES];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -79,54 +93,33 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
     const Tile t = decode_tile<BM, BN>(p);
     const int m0 = t.m0, n0 = t.n0;
     const float* __restrict__ A = p.A + (int64_t)t.bz * p.stride_a;
-    const uint16_t* __restrict__ Wx = p.Wx;
-    const int64_t plane_stride = (int64_t)p.N * p.Kp;
+    const char* __restrict__ Wf = reinterpret_cast<const char*>(p.Wx);
+    const int KS = p.Kp / 16;
+    const int NT = (p.N + 31) / 32;
+    const int nk = p.Kp / BK;
 
-    float4 ra[A_LOADS];
-    uint4 rw[W_LOADS];
-
-    auto load_tile = [&](int k0) {
+    // LDS-DMA sources.  A piece j = rows 8j .. 8j+7; lane -> (row 8j + lane/8, position lane%8)
+    // holding chunk position ^ f(row).  Rows past M re-read row M-1 and chunks past K re-read
+    // chunk 0 (finite data; the W planes are zero there and those rows are never stored).
+    const int prow = lane >> 3, ppos = lane & 7;
+    auto issue = [&](int kt, char* abuf, char* wbuf) {
+        const int k0 = kt * BK;
 #pragma unroll
-        for (int i = 0; i < A_LOADS; ++i) {
-            const int q = tid + 256 * i;
-            const int row = q >> 3, c = (q & 7) * 4;
-            const int gm = m0 + row, gk = k0 + c;
-            ra[i] = (gm < p.M && gk < p.K) ? *reinterpret_cast<const float4*>(A + (int64_t)gm * p.lda + gk)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int jj = 0; jj < A_INSTR / 4; ++jj) {
+            const int j = jj * 4 + wave;
+            const int row = j * 8 + prow;
+            const int gm = min(m0 + row, p.M - 1);
+            const int gk = k0 + 4 * (ppos ^ a_swz(row));
+            const float* src = A + (int64_t)gm * p.lda + (gk < p.K ? gk : 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (lds_void*)(abuf + j * 1024), 16, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < W_LOADS; ++i) {
-            const int q = tid + 256 * i;  // (plane, row, chunk)
-            const int pl = q / (BN * 4), rem = q % (BN * 4);
-            const int row = rem >> 2, c = rem & 3;
-            const int gn = n0 + row;
-            rw[i] = gn < p.N ? *reinterpret_cast<const uint4*>(Wx + pl * plane_stride + (int64_t)gn * p.Kp + k0 + c * 8)
-                             : make_uint4(0, 0, 0, 0);
-        }
-    };
-    auto store_tile = [&]() {
-#pragma unroll
-        for (int i = 0; i < A_LOADS; ++i) {
-            const int q = tid + 256 * i;
-            const int row = q >> 3, c4 = q & 7;  // float4 c4 = half (c4 & 1) of chunk c4 >> 1
-            const int off = swz(row, c4 >> 1) + 8 * (c4 & 1);
-            bf16x4 hi, mid, lo;
-            if constexpr (VASR_X3_ABLATE & 4) {
-                hi = bf16x4{(__bf16)ra[i].x, (__bf16)ra[i].y, (__bf16)ra[i].z, (__bf16)ra[i].w};
-                mid = hi;
-                lo = hi;
-            } else {
-                split4(ra[i], hi, mid, lo);
-            }
-            *reinterpret_cast<bf16x4*>(As + off) = hi;
-            *reinterpret_cast<bf16x4*>(As + A_PLANE + off) = mid;
-            *reinterpret_cast<bf16x4*>(As + 2 * A_PLANE + off) = lo;
-        }
-#pragma unroll
-        for (int i = 0; i < W_LOADS; ++i) {
-            const int q = tid + 256 * i;
-            const int pl = q / (BN * 4), rem = q % (BN * 4);
-            *reinterpret_cast<uint4*>(Ws + pl * W_PLANE + swz(rem >> 2, rem & 3)) = rw[i];
+        for (int jj = 0; jj < W_INSTR / 4; ++jj) {
+            const int j = jj * 4 + wave;
+            const int tnl = j / 6, rem = j - tnl * 6;  // rem = k-step * 3 + plane
+            const int nt = min(n0 / 32 + tnl, NT - 1);
+            const char* src = Wf + ((int64_t)(nt * KS + 2 * kt) * 3 + rem) * 1024 + lane * 16;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (lds_void*)(wbuf + j * 1024), 16, 0, 0);
         }
     };
 
@@ -138,30 +131,25 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[tm][tn][i] = 0.f;
 
-    const int nk = (p.K + BK - 1) / BK;
-    load_tile(0);
-    store_tile();
-    __syncthreads();
-
-    const int a_row = wr * 32 * TM + r;
-    const int w_row = wc * 32 * TN + r;
-
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk && !((VASR_X3_ABLATE & 8) && kt > 0)) load_tile((kt + 1) * BK);
+    const int fr = a_swz(r);
+    auto compute = [&](const char* abuf, const char* wbuf) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            const int chunk = 2 * s + h;
+            const int c0 = 4 * s + 2 * h;
             bf16x8 fa[3][TM], fw[3][TN];
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm)
-                    fa[pl][tm] = *reinterpret_cast<const bf16x8*>(As + pl * A_PLANE + swz(a_row + tm * 32, chunk));
-#pragma unroll
-                for (int tn = 0; tn < TN; ++tn)
-                    fw[pl][tn] = *reinterpret_cast<const bf16x8*>(Ws + pl * W_PLANE + swz(w_row + tn * 32, chunk));
+            for (int tm = 0; tm < TM; ++tm) {
+                const char* rowp = abuf + (wr * 32 * TM + tm * 32 + r) * (BK * 4);
+                const float4 x0 = *reinterpret_cast<const float4*>(rowp + 16 * (c0 ^ fr));
+                const float4 x1 = *reinterpret_cast<const float4*>(rowp + 16 * ((c0 + 1) ^ fr));
+                split8(x0, x1, fa[0][tm], fa[1][tm], fa[2][tm]);
             }
-            // small terms first, then the leading hi*hi term
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    fw[pl][tn] = *reinterpret_cast<const bf16x8*>(wbuf + (((wc * TN + tn) * 2 + s) * 3 + pl) * 1024 +
+                                                                  lane * 16);
             if constexpr (VASR_X3_ABLATE & 1) {
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
@@ -169,6 +157,7 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
                     for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)fa[0][tm][0] * (float)fw[2][tn][1];
                 continue;
             }
+            // small terms first, then the leading hi*hi term
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -183,11 +172,18 @@ __global__ __launch_bounds__(256) void gemm_x3_kernel(GemmParams p) {
                     acc[tm][tn] = c;
                 }
         }
+    };
+
+    issue(0, a0, w0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+        if (kt + 1 < nk) issue(kt + 1, a1, w1);
+        compute(a0, w0);
+        __syncthreads();  // stage kt+1 landed (vmcnt(0)); every wave is done with a0/w0
+        if (kt + 1 >= nk) break;
+        if (kt + 2 < nk) issue(kt + 2, a0, w0);
+        compute(a1, w1);
         __syncthreads();
-        if (kt + 1 < nk) {
-            store_tile();
-            __syncthreads();
-        }
     }
 
     if constexpr (VASR_X3_ABLATE & 2) {  // keep every accumulator live, store nothing
@@ -229,36 +225,40 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     return launch_status("vasr_linear_x3_f32");
 }
 
-// occ: min(waves per SIMD from VGPR+AGPR use, 160 KiB / LDS per block)
+// occ: min(waves per SIMD from the register use, 160 KiB / LDS per block)
 constexpr TileCfg kCfgs[] = {
-    {2, 2, 2, 2, 2},  // 128 x 128: 200 regs, 48 KiB
-    {2, 2, 1, 2, 3},  //  64 x 128: 132 regs, 36 KiB
-    {4, 1, 1, 2, 3},  // 128 x  64
-    {2, 2, 1, 1, 5},  //  64 x  64:  82 regs, 24 KiB
+    {2, 2, 2, 2, 2},  // 128 x 128: 250 regs, 80 KiB
+    {2, 2, 1, 2, 2},  //  64 x 128: 152 regs, 64 KiB
+    {4, 1, 1, 2, 2},  // 128 x  64: 144 regs, 56 KiB
+    {2, 2, 1, 1, 4},  //  64 x  64: 100 regs, 40 KiB
 };
 
-// [3][N][Kp] planes; thread per 8 consecutive k of one row.
+// Fragment-native planes [NT][KS][3][64][8] (NT = ceil(N/32), KS = Kp/16): element (n, k)
+// sits in tile n/32, k-step k/16, lane 32*((k%16)/8) + n%32, slot k%8.  One thread per 8
+// consecutive k of one (padded) row; rows >= N and k >= K are zero.
 __global__ void split_weights_kernel(const float* __restrict__ W, int64_t ldw, int N, int K, int Kp,
                                      uint16_t* __restrict__ out) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int cpr = Kp / 8;
-    if (q >= (int64_t)N * cpr) return;
+    const int NT = (N + 31) / 32;
+    if (q >= (int64_t)NT * 32 * cpr) return;
     const int n = (int)(q / cpr), k0 = (int)(q % cpr) * 8;
     bf16x8 hi, mid, lo;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const float x = k0 + j < K ? W[(int64_t)n * ldw + k0 + j] : 0.0f;
-        const __bf16 a = (__bf16)x;
-        const float r1 = x - (float)a;
-        const __bf16 b = (__bf16)r1;
+        const float x = (n < N && k0 + j < K) ? W[(int64_t)n * ldw + k0 + j] : 0.0f;
+        __bf16 a, b, c;
+        split1(x, a, b, c);
         hi[j] = a;
         mid[j] = b;
-        lo[j] = (__bf16)(r1 - (float)b);
+        lo[j] = c;
     }
-    const int64_t plane = (int64_t)N * Kp, base = (int64_t)n * Kp + k0;
+    const int KS = Kp / 16;
+    const int lane = 32 * ((k0 % 16) / 8) + n % 32;
+    const int64_t base = ((int64_t)(n / 32) * KS + k0 / 16) * 3 * 512 + lane * 8;
     *reinterpret_cast<bf16x8*>(out + base) = hi;
-    *reinterpret_cast<bf16x8*>(out + plane + base) = mid;
-    *reinterpret_cast<bf16x8*>(out + 2 * plane + base) = lo;
+    *reinterpret_cast<bf16x8*>(out + base + 512) = mid;
+    *reinterpret_cast<bf16x8*>(out + base + 1024) = lo;
 }
 
 }  // namespace
@@ -266,7 +266,7 @@ __global__ void split_weights_kernel(const float* __restrict__ W, int64_t ldw, i
 
 VASR_API int64_t vasr_split_weights_elems(int N, int K) {
     if (N <= 0 || K <= 0) return 0;
-    return 3 * (int64_t)N * ((K + 31) / 32 * 32);
+    return 3 * (int64_t)((N + 31) / 32 * 32) * ((K + 31) / 32 * 32);
 }
 
 VASR_API int vasr_split_weights_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream) {
@@ -276,7 +276,7 @@ VASR_API int vasr_split_weights_bf16x3(const float* W, int64_t ldw, int N, int K
                    (long long)ldw);
     VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "vasr_split_weights_bf16x3: out must be 16-byte aligned");
     const int Kp = (K + 31) / 32 * 32;
-    const int64_t n = (int64_t)N * (Kp / 8);
+    const int64_t n = (int64_t)((N + 31) / 32 * 32) * (Kp / 8);
     hipLaunchKernelGGL(split_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), W, ldw,
                        N, K, Kp, out);
     return launch_status("vasr_split_weights_bf16x3");
