@@ -61,9 +61,9 @@ __device__ __forceinline__ Tile decode_tile(const GemmParams& p) {
 // Accumulator element i of MFMA tile (tm, tn) of wave (wr, wc), lane (r, h) is
 // C[m0 + wr*32*TM + tm*32 + (i&3) + 8*(i>>2) + 4*h][n0 + wc*32*TN + tn*32 + r].
 //
-// The "pair" epilogues rely on the two 32-column MFMA tiles of a wave (tn = 0, 1) holding
-// two views of the same 32 output columns in the same lane and register: PAIR_POWER puts
-// DFT cos|sin rows side by side (|X|^2 in-register); PAIR_FUSION puts the gate and
+// The "pair" epilogues rely on each pair of 32-column MFMA tiles of a wave (tn = 2tp, 2tp+1)
+// holding two views of the same 32 output columns in the same lane and register: PAIR_POWER
+// puts DFT cos|sin rows side by side (|X|^2 in-register); PAIR_FUSION puts the gate and
 // global_proj rows side by side (gated fusion in-register).
 //
 // GUARD = false for tiles wholly inside M x N: no per-element bounds branches.
@@ -75,35 +75,38 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
     const int m0 = t.m0, n0 = t.n0;
 
     if constexpr (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) {
-        const int col = (n0 + wc * 32 * TN) / 2 + r;  // output column of this lane
-        if (GUARD && col >= p.n_out) return;
-        float bg = 0.f, bgl = 0.f, b2 = 0.f;
-        const int pc = n0 + wc * 32 * TN + r;  // paired column of half 0
-        if constexpr (EPI == VASR_EPI_PAIR_FUSION) {
-            bg = p.bias[pc];
-            bgl = p.bias[pc + 32];
-            b2 = p.aux2[col];
-        }
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
+        for (int tp = 0; tp < TN / 2; ++tp) {
+            const int col = (n0 + wc * 32 * TN) / 2 + tp * 32 + r;  // output column of this lane
+            if (GUARD && col >= p.n_out) continue;
+            const int pc = n0 + wc * 32 * TN + tp * 64 + r;  // paired column of half 0
+            float bg = 0.f, bgl = 0.f, b2 = 0.f;
+            if constexpr (EPI == VASR_EPI_PAIR_FUSION) {
+                bg = p.bias[pc];
+                bgl = p.bias[pc + 32];
+                b2 = p.aux2[col];
+            }
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (GUARD && row >= p.M) continue;
-                const float v0 = acc[tm][0][i];
-                const float v1 = acc[tm][TN - 1][i];
-                float out;
-                if constexpr (EPI == VASR_EPI_PAIR_POWER) {
-                    out = v0 * v0 + v1 * v1;
-                } else {
-                    // aux: local-side partial products in the same paired layout.
-                    const float* ar = auxb + (int64_t)row * p.ld_aux;
-                    const float gate = sigmoid_fast((ar[pc] + v0) + bg);
-                    const float lt = ar[pc + 32] + b2;
-                    const float gt = v1 + bgl;
-                    out = gate * lt + (1.0f - gate) * gt;
+            for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (GUARD && row >= p.M) continue;
+                    const float v0 = acc[tm][2 * tp][i];
+                    const float v1 = acc[tm][2 * tp + 1][i];
+                    float out;
+                    if constexpr (EPI == VASR_EPI_PAIR_POWER) {
+                        out = v0 * v0 + v1 * v1;
+                    } else {
+                        // aux: local-side partial products in the same paired layout.
+                        const float* ar = auxb + (int64_t)row * p.ld_aux;
+                        const float gate = sigmoid_fast((ar[pc] + v0) + bg);
+                        const float lt = ar[pc + 32] + b2;
+                        const float gt = v1 + bgl;
+                        out = gate * lt + (1.0f - gate) * gt;
+                    }
+                    Cb[(int64_t)row * p.ldc + col] = out;
                 }
-                Cb[(int64_t)row * p.ldc + col] = out;
             }
         }
     } else {
@@ -167,7 +170,7 @@ inline int pick_cfg(const TileCfg* cfgs, int n, int M, int N, int batch, bool pa
     double best_cost = 0;
     for (int i = 0; i < n; ++i) {
         const TileCfg& c = cfgs[i];
-        if (pair && c.tn != 2) continue;
+        if (pair && c.tn % 2 != 0) continue;
         const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
         const long per_cu = (tiles + kCUs - 1) / kCUs;
         const long rounds = (per_cu + c.occ - 1) / c.occ;

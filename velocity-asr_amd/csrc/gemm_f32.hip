@@ -24,7 +24,7 @@ template <int WM, int WN, int TM, int TN, int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
-    static_assert(TN == 2 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need TN=2");
+    static_assert(TN % 2 == 0 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need even TN");
     constexpr int A_LOADS = BM * (BK / 4) / 256;  // float4 per thread
     constexpr int W_LOADS = BN * (BK / 4) / 256;
     static_assert(A_LOADS >= 1 && W_LOADS >= 1, "tile too small");
@@ -148,10 +148,10 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
         case VASR_EPI_RESIDUAL: VASR_L(VASR_EPI_RESIDUAL); break;
         case VASR_EPI_GELU_PE: VASR_L(VASR_EPI_GELU_PE); break;
         case VASR_EPI_PAIR_POWER:
-            if constexpr (TN == 2) { VASR_L(VASR_EPI_PAIR_POWER); break; }
+            if constexpr (TN % 2 == 0) { VASR_L(VASR_EPI_PAIR_POWER); break; }
             set_error("vasr_linear_f32: paired epilogue needs a TN=2 tile"); return VASR_EINVAL;
         case VASR_EPI_PAIR_FUSION:
-            if constexpr (TN == 2) { VASR_L(VASR_EPI_PAIR_FUSION); break; }
+            if constexpr (TN % 2 == 0) { VASR_L(VASR_EPI_PAIR_FUSION); break; }
             set_error("vasr_linear_f32: paired epilogue needs a TN=2 tile"); return VASR_EINVAL;
         default: set_error("vasr_linear_f32: unknown epilogue %d", epi); return VASR_EINVAL;
     }

@@ -28,6 +28,8 @@
 // Operand maps (cdna_hip_programming.md §3): lane (r = lane & 31, h = lane >> 5) supplies
 // A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7.  The accumulator layout equals the
 // f32-input MFMA's, so gemm_common.h's epilogues apply.
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace vasr {
@@ -38,8 +40,8 @@ using namespace gemm;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifndef VASR_X3_ABLATE
-#define VASR_X3_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no C stores
-#endif
+#define VASR_X3_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no C stores, 4 no A split,
+#endif                    // 8 no LDS-DMA after the first stage, 16 no per-stage barrier
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -66,21 +68,47 @@ __device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x
     }
 }
 
-template <int WM, int WN, int TM, int TN, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
+// LDS-DMA of 16 B per lane into dst_base + 16*lane, issued from inline asm: the compiler then
+// does not track it, so it adds no waits of its own before reads of other ring slots (its
+// tracking loses the slot distinction across the loop back edge and drains the ring).  The
+// kernel orders these loads itself: counted vmcnt + barrier before a slot is read.  Extra
+// untracked vector-memory operations can only make the compiler's own vmcnt waits stricter.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16(const void* src, void* dst_base) {
+    const unsigned lds = (unsigned)(uintptr_t)(lds_void*)dst_base;
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// vmcnt(n) with lgkmcnt / expcnt left open (gfx9 s_waitcnt encoding).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int WM, int WN, int TM, int TN, int RING, int EPI>
+__global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <= 81920 ? 2 : 1) void gemm_x3_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
     static_assert(WM * WN == 4, "4 waves");
-    static_assert(TN == 2 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need TN=2");
+    static_assert(TN % 2 == 0 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need even TN");
     constexpr int A_BYTES = BM * BK * 4;            // fp32 [BM][32]
     constexpr int W_BYTES = (BN / 32) * 6 * 1024;   // [BN/32][2 k-steps][3 planes][64][16 B]
     constexpr int A_INSTR = A_BYTES / 1024, W_INSTR = W_BYTES / 1024;
     static_assert(A_INSTR % 4 == 0 && W_INSTR % 4 == 0, "whole LDS-DMA pieces per wave");
 
-    __shared__ __attribute__((aligned(16))) char a0[A_BYTES];
-    __shared__ __attribute__((aligned(16))) char w0[W_BYTES];
-    __shared__ __attribute__((aligned(16))) char a1[A_BYTES];
-    __shared__ __attribute__((aligned(16))) char w1[W_BYTES];
+    // RING stages, each one distinct LDS object [A | W] (unused ones are 16-B stubs).  One object
+    // per stage keeps the count of distinct LDS-DMA targets small enough for the compiler's
+    // waitcnt tracking to tell them apart (it then waits for nothing before a stage's reads).
+    static_assert(RING >= 2 && RING <= 4, "ring depth");
+    constexpr int STAGE = A_BYTES + W_BYTES;
+    __shared__ __attribute__((aligned(16))) char s0[STAGE];
+    __shared__ __attribute__((aligned(16))) char s1[STAGE];
+    __shared__ __attribute__((aligned(16))) char s2[RING > 2 ? STAGE : 16];
+    __shared__ __attribute__((aligned(16))) char s3[RING > 3 ? STAGE : 16];
+    constexpr int GL = (A_INSTR + W_INSTR) / 4;  // LDS-DMA instructions per wave per stage
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -98,28 +126,43 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     const int NT = (p.N + 31) / 32;
     const int nk = p.Kp / BK;
 
-    // LDS-DMA sources.  A piece j = rows 8j .. 8j+7; lane -> (row 8j + lane/8, position lane%8)
-    // holding chunk position ^ f(row).  Rows past M re-read row M-1 and chunks past K re-read
+    // LDS-DMA sources.  A piece j = rows 8j .. 8j+7 of the tile; lane -> (row 8j + lane/8,
+    // position lane%8) holding chunk position ^ f(row).  f(row) depends on the lane and on the
+    // parity of j only, so a lane's byte offset inside a piece takes two values; the piece and
+    // k-tile bases are wave-uniform.  Rows past M re-read row M-1 and chunks past K re-read
     // chunk 0 (finite data; the W planes are zero there and those rows are never stored).
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     const int prow = lane >> 3, ppos = lane & 7;
+    const int csw = ppos ^ ((prow >> 1) & 3);
+    const int a_off[2] = {csw * 16, (csw ^ 4) * 16};  // chunk byte offset in the row, j even / odd
+    const bool m_full = m0 + BM <= p.M;
+    const char* __restrict__ Ab = reinterpret_cast<const char*>(A);
+    const int64_t lda_b = p.lda * 4;
     auto issue = [&](int kt, char* abuf, char* wbuf) {
-        const int k0 = kt * BK;
+        if ((VASR_X3_ABLATE & 8) && kt > 0) return;
+        const int k0b = kt * BK * 4;
+        const bool k_full = (kt + 1) * BK <= p.K;
 #pragma unroll
         for (int jj = 0; jj < A_INSTR / 4; ++jj) {
-            const int j = jj * 4 + wave;
-            const int row = j * 8 + prow;
-            const int gm = min(m0 + row, p.M - 1);
-            const int gk = k0 + 4 * (ppos ^ a_swz(row));
-            const float* src = A + (int64_t)gm * p.lda + (gk < p.K ? gk : 0);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (lds_void*)(abuf + j * 1024), 16, 0, 0);
+            const int j = jj * 4 + wave_u;
+            int off = a_off[j & 1];
+            if (!k_full && k0b + off >= p.K * 4) off = 0;
+            const char* src;
+            if (m_full) {
+                src = Ab + (int64_t)(m0 + j * 8) * lda_b + k0b + prow * lda_b + off;
+            } else {
+                const int gm = min(m0 + j * 8 + prow, p.M - 1);
+                src = Ab + (int64_t)gm * lda_b + k0b + off;
+            }
+            glds16(src, abuf + j * 1024);
         }
 #pragma unroll
         for (int jj = 0; jj < W_INSTR / 4; ++jj) {
-            const int j = jj * 4 + wave;
+            const int j = jj * 4 + wave_u;
             const int tnl = j / 6, rem = j - tnl * 6;  // rem = k-step * 3 + plane
             const int nt = min(n0 / 32 + tnl, NT - 1);
             const char* src = Wf + ((int64_t)(nt * KS + 2 * kt) * 3 + rem) * 1024 + lane * 16;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (lds_void*)(wbuf + j * 1024), 16, 0, 0);
+            glds16(src, wbuf + j * 1024);
         }
     };
 
@@ -132,30 +175,51 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
             for (int i = 0; i < 16; ++i) acc[tm][tn][i] = 0.f;
 
     const int fr = a_swz(r);
+    // One stage = two MFMA k-steps.  All fragment reads of the stage are issued first, then
+    // step 0's A fragments are split and its MFMAs issued; step 1's split is independent VALU
+    // work the scheduler places in the shadow of step 0's MFMAs.
     auto compute = [&](const char* abuf, const char* wbuf) {
+        float4 xa[2][TM][2];
+        bf16x8 fw[2][3][TN];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int c0 = 4 * s + 2 * h;
-            bf16x8 fa[3][TM], fw[3][TN];
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
                 const char* rowp = abuf + (wr * 32 * TM + tm * 32 + r) * (BK * 4);
-                const float4 x0 = *reinterpret_cast<const float4*>(rowp + 16 * (c0 ^ fr));
-                const float4 x1 = *reinterpret_cast<const float4*>(rowp + 16 * ((c0 + 1) ^ fr));
-                split8(x0, x1, fa[0][tm], fa[1][tm], fa[2][tm]);
+                xa[s][tm][0] = *reinterpret_cast<const float4*>(rowp + 16 * (c0 ^ fr));
+                xa[s][tm][1] = *reinterpret_cast<const float4*>(rowp + 16 * ((c0 + 1) ^ fr));
             }
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl)
-                    fw[pl][tn] = *reinterpret_cast<const bf16x8*>(wbuf + (((wc * TN + tn) * 2 + s) * 3 + pl) * 1024 +
-                                                                  lane * 16);
+                    fw[s][pl][tn] = *reinterpret_cast<const bf16x8*>(
+                        wbuf + (((wc * TN + tn) * 2 + s) * 3 + pl) * 1024 + lane * 16);
+        }
+        bf16x8 fa[2][3][TM];
+        auto split_step = [&](int s) {
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+                if constexpr (VASR_X3_ABLATE & 4) {
+                    const float4 x0 = xa[s][tm][0], x1 = xa[s][tm][1];
+                    const bf16x8 v = {(__bf16)x0.x, (__bf16)x0.y, (__bf16)x0.z, (__bf16)x0.w,
+                                      (__bf16)x1.x, (__bf16)x1.y, (__bf16)x1.z, (__bf16)x1.w};
+                    fa[s][0][tm] = v;
+                    fa[s][1][tm] = v;
+                    fa[s][2][tm] = v;
+                } else {
+                    split8(xa[s][tm][0], xa[s][tm][1], fa[s][0][tm], fa[s][1][tm], fa[s][2][tm]);
+                }
+            }
+        };
+        auto mfma_step = [&](int s) {
             if constexpr (VASR_X3_ABLATE & 1) {
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)fa[0][tm][0] * (float)fw[2][tn][1];
-                continue;
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)fa[s][0][tm][0] * (float)fw[s][2][tn][1];
+                return;
             }
             // small terms first, then the leading hi*hi term
 #pragma unroll
@@ -163,28 +227,65 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
                     floatx16 c = acc[tm][tn];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2][tm], fw[0][tn], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][tm], fw[2][tn], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][tm], fw[1][tn], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][tm], fw[0][tn], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][tm], fw[1][tn], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][tm], fw[0][tn], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][2][tm], fw[s][0][tn], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][tm], fw[s][2][tn], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][1][tm], fw[s][1][tn], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][1][tm], fw[s][0][tn], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][tm], fw[s][1][tn], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][tm], fw[s][0][tn], c, 0, 0, 0);
                     acc[tm][tn] = c;
                 }
-        }
+        };
+        split_step(0);
+        mfma_step(0);
+        split_step(1);
+        mfma_step(1);
     };
 
-    issue(0, a0, w0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-        if (kt + 1 < nk) issue(kt + 1, a1, w1);
-        compute(a0, w0);
-        __syncthreads();  // stage kt+1 landed (vmcnt(0)); every wave is done with a0/w0
+    // Ring pipeline: stage kt lives in slot kt % RING; up to RING-1 stages are in flight.  Each
+    // step waits for its own stage with a counted vmcnt (the LDS-DMA instructions per wave and
+    // stage are a compile-time count, and nothing else touches the vector-memory counter in the
+    // loop), then a raw barrier publishes it block-wide and certifies that every wave is done
+    // reading the slot the step refills.
+    auto slot = [&](auto Ic) -> char* {
+        constexpr int I = decltype(Ic)::value;
+        if constexpr (I == 0) return s0;
+        else if constexpr (I == 1) return s1;
+        else if constexpr (I == 2) return s2;
+        else return s3;
+    };
+    // Every step issues exactly GL LDS-DMA instructions (past the last stage it re-loads stage
+    // nk-1 into the slot it frees, which nothing reads again), so one wait count serves all
+    // steps: vmcnt((RING-2)*GL) leaves the RING-2 younger stages in flight.  The prologue fills
+    // RING-1 stages the same way.
+    auto step = [&](auto Ic, int kt) {
+        constexpr int I = decltype(Ic)::value;
+        constexpr int NEXT = (I + RING - 1) % RING;
+        wait_vmcnt<(RING - 2) * GL>();
+        if constexpr (!(VASR_X3_ABLATE & 16)) __builtin_amdgcn_s_barrier();
+        char* nb = slot(std::integral_constant<int, NEXT>());
+        issue(min(kt + RING - 1, nk - 1), nb, nb + A_BYTES);
+        char* cb = slot(Ic);
+        compute(cb, cb + A_BYTES);
+    };
+
+    issue(0, s0, s0 + A_BYTES);
+    if constexpr (RING > 2) issue(min(1, nk - 1), s1, s1 + A_BYTES);
+    if constexpr (RING > 3) issue(min(2, nk - 1), s2, s2 + A_BYTES);
+    for (int kt = 0; kt < nk; kt += RING) {
+        step(std::integral_constant<int, 0>(), kt);
         if (kt + 1 >= nk) break;
-        if (kt + 2 < nk) issue(kt + 2, a0, w0);
-        compute(a1, w1);
-        __syncthreads();
+        step(std::integral_constant<int, 1>(), kt + 1);
+        if constexpr (RING > 2) {
+            if (kt + 2 >= nk) break;
+            step(std::integral_constant<int, 2>(), kt + 2);
+        }
+        if constexpr (RING > 3) {
+            if (kt + 3 >= nk) break;
+            step(std::integral_constant<int, 3>(), kt + 3);
+        }
     }
+    __syncthreads();  // LDS no longer read (the epilogue does not use it); drain for safety
 
     if constexpr (VASR_X3_ABLATE & 2) {  // keep every accumulator live, store nothing
         float sum = 0.f;
@@ -199,14 +300,14 @@ __global__ __launch_bounds__(256, 2) void gemm_x3_kernel(GemmParams p) {
     epilogue<BM, BN, TM, TN, EPI>(p, t, acc, wr, wc, r, h);
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int RING>
 int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
     const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
     dim3 grid(tiles, batch);
     dim3 block(256);
-#define VASR_L(E) hipLaunchKernelGGL((gemm_x3_kernel<WM, WN, TM, TN, E>), grid, block, 0, s, p)
+#define VASR_L(E) hipLaunchKernelGGL((gemm_x3_kernel<WM, WN, TM, TN, RING, E>), grid, block, 0, s, p)
     switch (epi) {
         case VASR_EPI_NONE: VASR_L(VASR_EPI_NONE); break;
         case VASR_EPI_GELU: VASR_L(VASR_EPI_GELU); break;
@@ -214,24 +315,41 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
         case VASR_EPI_RESIDUAL: VASR_L(VASR_EPI_RESIDUAL); break;
         case VASR_EPI_GELU_PE: VASR_L(VASR_EPI_GELU_PE); break;
         case VASR_EPI_PAIR_POWER:
-            if constexpr (TN == 2) { VASR_L(VASR_EPI_PAIR_POWER); break; }
-            set_error("vasr_linear_x3_f32: paired epilogue needs a TN=2 tile"); return VASR_EINVAL;
+            if constexpr (TN % 2 == 0) { VASR_L(VASR_EPI_PAIR_POWER); break; }
+            set_error("vasr_linear_x3_f32: paired epilogue needs an even TN"); return VASR_EINVAL;
         case VASR_EPI_PAIR_FUSION:
-            if constexpr (TN == 2) { VASR_L(VASR_EPI_PAIR_FUSION); break; }
-            set_error("vasr_linear_x3_f32: paired epilogue needs a TN=2 tile"); return VASR_EINVAL;
+            if constexpr (TN % 2 == 0) { VASR_L(VASR_EPI_PAIR_FUSION); break; }
+            set_error("vasr_linear_x3_f32: paired epilogue needs an even TN"); return VASR_EINVAL;
         default: set_error("vasr_linear_x3_f32: unknown epilogue %d", epi); return VASR_EINVAL;
     }
 #undef VASR_L
     return launch_status("vasr_linear_x3_f32");
 }
 
-// occ: min(waves per SIMD from the register use, 160 KiB / LDS per block)
+// Tile shapes, largest first.  Measured (tools/gemm_variant_sweep.py, M = 16032): the
+// 128 x 128 tile has the best main loop (1.0 : 0.89 for 128 x 64 : 0.76 for 64 x 64 at long K)
+// and wins whenever it still yields about two tiles per CU; below that the CU balance of the
+// smaller tiles wins.  occ: min(waves per SIMD from the register use, 160 KiB / LDS per block).
+#ifndef VASR_X3_RING
+#define VASR_X3_RING 2  // deeper rings (3, 4) measured slower: they cost a block per CU
+#endif
+constexpr int RING_SMALL = VASR_X3_RING;                      // 64 x 64 tiles
+constexpr int RING_BIG = VASR_X3_RING > 3 ? 3 : VASR_X3_RING;  // larger tiles
 constexpr TileCfg kCfgs[] = {
-    {2, 2, 2, 2, 2},  // 128 x 128: 250 regs, 80 KiB
-    {2, 2, 1, 2, 2},  //  64 x 128: 152 regs, 64 KiB
-    {4, 1, 1, 2, 2},  // 128 x  64: 144 regs, 56 KiB
-    {2, 2, 1, 1, 4},  //  64 x  64: 100 regs, 40 KiB
+    {2, 2, 2, 2, 2},  // 128 x 128
+    {4, 1, 1, 2, 2},  // 128 x  64
+    {2, 2, 1, 1, 4},  //  64 x  64
 };
+
+int pick_x3(int M, int N, int batch, bool pair) {
+    for (int i = 0; i < 2; ++i) {
+        const TileCfg& c = kCfgs[i];
+        const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
+        const bool exact_n = N % c.bn() == 0 || N > 4 * c.bn();  // little padding waste
+        if (tiles >= 19 * kCUs / 10 && exact_n) return i;
+    }
+    return pair ? 1 : 2;  // paired epilogues need an even TN
+}
 
 // Fragment-native planes [NT][KS][3][64][8] (NT = ceil(N/32), KS = Kp/16): element (n, k)
 // sits in tile n/32, k-step k/16, lane 32*((k%16)/8) + n%32, slot k%8.  One thread per 8
@@ -294,10 +412,14 @@ VASR_API int vasr_linear_x3_f32(const vasr_gemm_args* a, const uint16_t* w_split
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     hipStream_t s = as_stream(stream);
-    switch (pick_cfg(kCfgs, 4, a->M, a->N, a->batch, pair)) {
-        case 0: return launch_cfg<2, 2, 2, 2>(p, a->batch, epi, s);
-        case 1: return launch_cfg<2, 2, 1, 2>(p, a->batch, epi, s);
-        case 2: return launch_cfg<4, 1, 1, 2>(p, a->batch, epi, s);
-        default: return launch_cfg<2, 2, 1, 1>(p, a->batch, epi, s);
+#ifdef VASR_X3_FORCE_CFG
+    const int cfg = VASR_X3_FORCE_CFG;  // diagnostic builds only
+#else
+    const int cfg = pick_x3(a->M, a->N, a->batch, pair);
+#endif
+    switch (cfg) {
+        case 0: return launch_cfg<2, 2, 2, 2, RING_BIG>(p, a->batch, epi, s);
+        case 1: return launch_cfg<4, 1, 1, 2, RING_BIG>(p, a->batch, epi, s);
+        default: return launch_cfg<2, 2, 1, 1, RING_SMALL>(p, a->batch, epi, s);
     }
 }
