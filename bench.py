@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
     ap.add_argument("--streams", type=int, default=1, help="utterance groups replayed on concurrent HIP streams")
+    ap.add_argument("--int8", action="store_true",
+                    help="BASELINE configs[4]: INT8 fake-quant model (prepare_model_for_qat + activation calibration)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -133,6 +135,12 @@ def main():
     from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids
 
     model = build_model(dev)
+    if args.int8:
+        from velocity_asr import compute_mel_spectrogram
+        from velocity_asr import quantize as Q
+        model = Q.prepare_model_for_qat(model).to(dev).eval()
+        calib = torch.from_numpy(S.make_audio(2, 48000, seed=71)).to(dev)
+        Q.calibrate_from_activations(model, compute_mel_spectrogram(calib))
     S_len = int(args.seconds * SR)
     B = args.batch
     audio = torch.from_numpy(S.make_audio(B, S_len, seed=1234 + rank)).to(dev)  # resident in HBM
@@ -216,7 +224,9 @@ def main():
         "dtype": "f32",
         "data": "synthetic: N(0, 0.1) 16 kHz clips; seeded random-init weights (velocity_asr.synthetic)",
         "config": {"workload": f"{B} x {args.seconds:g} s clips per GPU, audio->mel->forward->CTC greedy tokens "
-                               f"(BASELINE configs[1]{f', HIP graph x{args.streams} streams' if not args.eager else ', eager'})",
+                               f"(BASELINE configs[{4 if args.int8 else 1}]"
+                               f"{', INT8 fake-quant' if args.int8 else ''}"
+                               f"{f', HIP graph x{args.streams} streams' if not args.eager else ', eager'})",
                    "global_batch": world * B, "clip_seconds": args.seconds, "parallelism": f"utterance-shard x{world}"},
         "frames_per_sec": round(frames / elapsed, 1),
         "roofline": roof,

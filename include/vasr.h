@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 2
+#define VASR_ABI_VERSION 3
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -75,6 +75,14 @@ typedef struct vasr_gemm_args {
     int64_t ld_aux, stride_aux;
     const float* aux2;      /* PAIR_FUSION: local_proj bias [n_out] */
     int32_t n_out;          /* PAIR_*: output columns; SOFTPLUS_FROM: first softplus column */
+    const float* qparams;   /* NULL, or per-column activation fake-quant {scale, zero_point,
+                               qmin, qmax} (4 floats per column) applied to acc + bias before
+                               the epilogue's function (QuantizedLinear / QuantizedConv1d
+                               activation_quantizer, quantize.py:177-191, :252-266).
+                               PAIR_FUSION: N entries in the paired column layout (gate |
+                               global_proj) followed by n_out entries for local_proj.
+                               A column whose scale is 0 is not quantized.  Not allowed
+                               with PAIR_POWER. */
 } vasr_gemm_args;
 
 int vasr_linear_f32(const vasr_gemm_args* args, void* stream);
@@ -170,6 +178,25 @@ int vasr_adaptive_pool_f32(const float* x, float* out, int B, int L, int C, int 
  */
 int vasr_pooled_attention_f32(const float* q, int64_t ld_q, const float* kv, float* out,
                               int B, int L, int Kp, int heads, int head_dim, void* stream);
+
+/* ------------------------------------------------------------------ INT8 fake quantisation (C5)
+ * FakeQuantize.forward in eval with calibrated buffers (quantize.py:79-97, :118-133):
+ *   q = clamp(round_half_even(x / scale + zp), qmin, qmax); x_dq = (q - zp) * scale;
+ *   y = x + (x_dq - x)
+ * every operation IEEE-rounded in that order (bit-identical to torch's CPU evaluation).
+ * x, y: (rows, cols) with row strides ldx, ldy (y may alias x).  scale / zero_point are
+ * device arrays of `rows` entries if per_row != 0 (per-output-channel weights,
+ * channel_dim 0) or of one entry (per-tensor).
+ */
+int vasr_fakequant_f32(const float* x, int64_t ldx, float* y, int64_t ldy, int rows, int cols,
+                       const float* scale, const float* zero_point, int per_row, float qmin,
+                       float qmax, void* stream);
+
+/* Per-row min and max of x (rows, cols), NaN-propagating like torch.amin / amax: the
+ * statistics FakeQuantize._update_scale_zp observes (quantize.py:99-116).  A per-tensor
+ * range is two calls (rows of x, then the row results as one row). */
+int vasr_minmax_f32(const float* x, int64_t ldx, int rows, int cols, float* out_min,
+                    float* out_max, void* stream);
 
 /* ------------------------------------------------------------------ CTC decode
  * argmax over V per row, ties -> first index (decode.py:46).

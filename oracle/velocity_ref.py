@@ -150,6 +150,73 @@ def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None) -> np.n
     return y
 
 
+# --------------------------------------------------------------------------- INT8 fake quant (C5)
+def fake_quantize(x: np.ndarray, scale, zero_point, qmin: float, qmax: float) -> np.ndarray:
+    """FakeQuantize.forward in eval with calibrated buffers (quantize.py:79-97): q =
+    clamp(round_half_even(x / scale + zp), qmin, qmax) (:118-124), x_dq = (q - zp) * scale
+    (:126-128), returned as x + (x_dq - x) (:97).  scale / zp broadcast (per-tensor or
+    per-output-channel)."""
+    x = np.asarray(x, f32)
+    s = np.asarray(scale, f32)
+    zp = np.asarray(zero_point, f32)
+    q = np.clip(np.rint((x / s).astype(f32) + zp), f32(qmin), f32(qmax)).astype(f32)
+    xdq = ((q - zp).astype(f32) * s).astype(f32)
+    return (x + (xdq - x).astype(f32)).astype(f32)
+
+
+def observe_scale_zp(x: np.ndarray, symmetric: bool, per_channel: bool, qmin: int, qmax: int):
+    """FakeQuantize._update_scale_zp (quantize.py:99-116), channel_dim 0."""
+    x = np.asarray(x, f32)
+    if per_channel:
+        axes = tuple(range(1, x.ndim))
+        lo, hi = x.min(axis=axes, keepdims=True), x.max(axis=axes, keepdims=True)
+    else:
+        lo, hi = x.min(), x.max()
+    lo, hi = np.asarray(lo, f32), np.asarray(hi, f32)
+    if symmetric:
+        scale = (np.maximum(np.abs(lo), np.abs(hi)) / f32(qmax)).astype(f32)
+        zp = np.zeros_like(scale)
+    else:
+        scale = ((hi - lo) / f32(qmax - qmin)).astype(f32)
+        zp = (f32(qmin) - (lo / scale).astype(f32)).astype(f32)
+    return np.maximum(scale, f32(1e-10)).astype(f32), zp
+
+
+def qat_params(state: Dict[str, np.ndarray], weight_bits: int = 8, activation_bits: int = 8,
+               symmetric_activations: bool = False) -> Dict[str, dict]:
+    """Quantizer buffers of a prepare_model_for_qat state_dict (quantize.py:269-322) ->
+    {module path: {"w": (scale, zp, qmin, qmax) or None, "a": ... or None}}; an
+    uncalibrated quantizer passes through in eval (quantize.py:82-84) and maps to None."""
+    wq = (-(2 ** (weight_bits - 1)), 2 ** (weight_bits - 1) - 1)
+    aq = ((-(2 ** (activation_bits - 1)), 2 ** (activation_bits - 1) - 1) if symmetric_activations
+          else (0, 2 ** activation_bits - 1))
+    out: Dict[str, dict] = {}
+    for k in state:
+        if not k.endswith(".weight_quantizer.scale"):
+            continue
+        path = k[: -len(".weight_quantizer.scale")]
+        ent = {}
+        for kind, qr, key in (("w", wq, "weight_quantizer"), ("a", aq, "activation_quantizer")):
+            pre = f"{path}.{key}."
+            cal = bool(np.asarray(state[pre + "calibrated"]))
+            ent[kind] = (np.asarray(state[pre + "scale"], f32), np.asarray(state[pre + "zero_point"], f32),
+                         qr[0], qr[1]) if cal else None
+        out[path] = ent
+    return out
+
+
+def qlinear(W, Q, path: str, x: np.ndarray) -> np.ndarray:
+    """nn.Linear, or QuantizedLinear.forward (quantize.py:177-191) when Q has `path`."""
+    w, b = W[path + ".weight"], W.get(path + ".bias")
+    q = Q.get(path) if Q else None
+    if q is None:
+        return linear(x, w, b)
+    if q["w"] is not None:
+        w = fake_quantize(w, *q["w"])
+    y = linear(x, w, b)
+    return fake_quantize(y, *q["a"]) if q["a"] is not None else y
+
+
 def conv1d_k3s2(x: np.ndarray, w: np.ndarray, b: np.ndarray) -> np.ndarray:
     """TemporalBindingLayer.conv (model.py:156-162): Conv1d(80->D, k3, s2, p1) on
     (B, F, C) input, returned as (B, L, D)."""
@@ -305,9 +372,17 @@ def ssm_block(W, p: str, x: np.ndarray, mode: str) -> np.ndarray:
     return (h + r).astype(f32)
 
 
-def temporal_binding(W, mel: np.ndarray) -> np.ndarray:
-    """TemporalBindingLayer.forward (model.py:176-202) + PositionalEncoding2D (:106-127)."""
-    x = gelu(conv1d_k3s2(mel, W["temporal_binding.conv.weight"], W["temporal_binding.conv.bias"]))
+def temporal_binding(W, mel: np.ndarray, Q=None) -> np.ndarray:
+    """TemporalBindingLayer.forward (model.py:176-202) + PositionalEncoding2D (:106-127);
+    with Q the conv is QuantizedConv1d (quantize.py:252-266)."""
+    w = W["temporal_binding.conv.weight"]
+    q = Q.get("temporal_binding.conv") if Q else None
+    if q is not None and q["w"] is not None:
+        w = fake_quantize(w, *q["w"])
+    x = conv1d_k3s2(mel, w, W["temporal_binding.conv.bias"])
+    if q is not None and q["a"] is not None:
+        x = fake_quantize(x, *q["a"])
+    x = gelu(x)
     L = x.shape[1]
     pe_t = W["temporal_binding.pos_encoding.pe_time"][:L]
     pe_f = np.broadcast_to(W["temporal_binding.pos_encoding.pe_freq"][0], (L, pe_t.shape[1]))
@@ -333,11 +408,11 @@ def adaptive_avg_pool(x: np.ndarray, K: int) -> np.ndarray:
     return out
 
 
-def multi_head_attention(W, p: str, q_in, kv_in, heads: int) -> np.ndarray:
+def multi_head_attention(W, p: str, q_in, kv_in, heads: int, Q=None) -> np.ndarray:
     """MultiHeadAttention.forward (attention.py:116-164), mask=None."""
-    q = linear(q_in, W[p + "q_proj.weight"], W[p + "q_proj.bias"])
-    k = linear(kv_in, W[p + "k_proj.weight"], W[p + "k_proj.bias"])
-    v = linear(kv_in, W[p + "v_proj.weight"], W[p + "v_proj.bias"])
+    q = qlinear(W, Q, p + "q_proj", q_in)
+    k = qlinear(W, Q, p + "k_proj", kv_in)
+    v = qlinear(W, Q, p + "v_proj", kv_in)
     B, Lq, A = q.shape
     hd = A // heads
     qh = q.reshape(B, Lq, heads, hd).transpose(0, 2, 1, 3)
@@ -348,46 +423,46 @@ def multi_head_attention(W, p: str, q_in, kv_in, heads: int) -> np.ndarray:
     e = np.exp(s).astype(f32)
     attn = (e / e.sum(axis=-1, keepdims=True)).astype(f32)
     o = np.matmul(attn, vh).astype(f32).transpose(0, 2, 1, 3).reshape(B, Lq, A)
-    return linear(o, W[p + "out_proj.weight"], W[p + "out_proj.bias"])
+    return qlinear(W, Q, p + "out_proj", o)
 
 
-def gated_fusion(W, p: str, local, glob) -> np.ndarray:
+def gated_fusion(W, p: str, local, glob, Q=None) -> np.ndarray:
     """GatedFusion.forward (attention.py:191-220)."""
-    g = sigmoid(linear(np.concatenate([local, glob], axis=-1), W[p + "gate_proj.0.weight"],
-                       W[p + "gate_proj.0.bias"]))
-    lt = linear(local, W[p + "local_proj.weight"], W[p + "local_proj.bias"])
-    gt = linear(glob, W[p + "global_proj.weight"], W[p + "global_proj.bias"])
+    g = sigmoid(qlinear(W, Q, p + "gate_proj.0", np.concatenate([local, glob], axis=-1)))
+    lt = qlinear(W, Q, p + "local_proj", local)
+    gt = qlinear(W, Q, p + "global_proj", glob)
     fused = (g * lt + (f32(1) - g) * gt).astype(f32)
-    return linear(fused, W[p + "out_proj.weight"], W[p + "out_proj.bias"])
+    return qlinear(W, Q, p + "out_proj", fused)
 
 
-def global_context(W, local: np.ndarray, cfg: dict) -> np.ndarray:
+def global_context(W, local: np.ndarray, cfg: dict, Q=None) -> np.ndarray:
     """HierarchicalGlobalContext.forward (attention.py:283-319)."""
     g = "global_context."
     L = local.shape[1]
     k1, _ = pool_sizes(L)
-    x = linear(adaptive_avg_pool(local, k1), W[g + "pool1.pool_proj.weight"], W[g + "pool1.pool_proj.bias"])
+    x = qlinear(W, Q, g + "pool1.pool_proj", adaptive_avg_pool(local, k1))
     for i in range(cfg["global_ssm_layers"]):
         x = ssm_block(W, f"{g}global_ssm.layers.{i}.", x, "parallel")   # GlobalSSM: always parallel
     x = layer_norm(x, W[g + "global_ssm.norm.weight"], W[g + "global_ssm.norm.bias"])
     k2 = min(min(64, max(16, k1 // 4)), x.shape[1])
-    x2 = linear(adaptive_avg_pool(x, k2), W[g + "pool2.pool_proj.weight"], W[g + "pool2.pool_proj.bias"])
+    x2 = qlinear(W, Q, g + "pool2.pool_proj", adaptive_avg_pool(x, k2))
     x2 = layer_norm(x2, W[g + "norm1.weight"], W[g + "norm1.bias"])
     q = layer_norm(local, W[g + "norm2.weight"], W[g + "norm2.bias"])
-    ctx = multi_head_attention(W, g + "cross_attention.", q, x2, cfg["attention_heads"])
-    return gated_fusion(W, g + "fusion.", local, ctx)
+    ctx = multi_head_attention(W, g + "cross_attention.", q, x2, cfg["attention_heads"], Q)
+    return gated_fusion(W, g + "fusion.", local, ctx, Q)
 
 
-def forward(W: Dict[str, np.ndarray], mel: np.ndarray, cfg: dict, return_features: bool = False):
-    """VELOCITYASR.forward (model.py:333-368): (B, F, mel_bins) -> (B, L, V)."""
-    x = temporal_binding(W, np.asarray(mel, f32))
+def forward(W: Dict[str, np.ndarray], mel: np.ndarray, cfg: dict, return_features: bool = False, Q=None):
+    """VELOCITYASR.forward (model.py:333-368): (B, F, mel_bins) -> (B, L, V).  Q (from
+    qat_params) runs the prepare_model_for_qat form of the model (C5)."""
+    x = temporal_binding(W, np.asarray(mel, f32), Q)
     tb = x
     for i in range(cfg["ssm_layers"]):
         x = ssm_block(W, f"local_ssm.layers.{i}.", x, cfg["scan_mode"])
     local = layer_norm(x, W["local_ssm.norm.weight"], W["local_ssm.norm.bias"])
-    fused = global_context(W, local, cfg)
+    fused = global_context(W, local, cfg, Q)
     h = layer_norm(fused, W["ctc_head.proj.0.weight"], W["ctc_head.proj.0.bias"])
-    logits = linear(h, W["ctc_head.proj.2.weight"], W["ctc_head.proj.2.bias"])
+    logits = qlinear(W, Q, "ctc_head.proj.2", h)
     if return_features:
         return logits, dict(temporal_binding=tb, local_features=local, fused_features=fused)
     return logits

@@ -304,8 +304,111 @@ def gen_decode():
     print("wrote decode.json")
 
 
+# --------------------------------------------------------------------------- int8 (C5)
+QAT_MAP_RE = (".linear.", ".conv.")
+
+
+def qat_state_from_fp32(qmodel, sd):
+    """The reference's prepare_model_for_qat re-initialises the replaced modules
+    (quantize.py:295-313, SURVEY a17 defect i); carry the fp32 weights over instead:
+    `X.linear.weight` / `X.conv.weight` take `X.weight`, quantizer buffers keep their init."""
+    out = {}
+    for k, v in qmodel.state_dict().items():
+        if k in sd:
+            out[k] = sd[k]
+            continue
+        for seg in QAT_MAP_RE:
+            head, _, tail = k.rpartition(seg)
+            if head and (head + "." + tail) in sd:
+                out[k] = sd[head + "." + tail]
+                break
+        else:
+            out[k] = v
+    return out
+
+
+def qat_model(calib_audio):
+    """fp32 weights in the reference's QAT modules, calibrated with the intended semantics:
+    weight quantizers on their weights, activation quantizers on the outputs of one
+    calibration forward (weights fake-quantized, activations still pass-through)."""
+    from velocity_asr.quantize import FakeQuantize, QuantizedConv1d, QuantizedLinear, prepare_model_for_qat
+    model = build_model()
+    sd = model.state_dict()
+    qmodel = prepare_model_for_qat(model)
+    qmodel.load_state_dict(qat_state_from_fp32(qmodel, sd), strict=True)
+    qmodel.eval()
+    qmods = {n: m for n, m in qmodel.named_modules() if isinstance(m, (QuantizedLinear, QuantizedConv1d))}
+    with torch.no_grad():
+        for n, m in qmods.items():
+            inner = m.linear if isinstance(m, QuantizedLinear) else m.conv
+            m.weight_quantizer.calibrate(inner.weight)
+        seen = {}
+        hooks = [m.register_forward_hook(lambda mod, inp, out, n=n: seen.__setitem__(n, out.detach().clone()))
+                 for n, m in qmods.items()]
+        mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(calib_audio))
+        qmodel(mel)
+        for h in hooks:
+            h.remove()
+        for n, m in qmods.items():
+            m.activation_quantizer.calibrate(seen[n])
+    return qmodel, sorted(qmods)
+
+
+def gen_int8():
+    calib = syn.make_audio(2, 48000, seed=71)
+    qmodel, names = qat_model(calib)
+    out = {}
+    for k, v in qmodel.state_dict().items():
+        if "quantizer" in k:
+            out["q__" + k] = v.numpy()
+    audio = syn.make_audio(2, 48000, seed=21)
+    mel, logits, feats = run_forward(qmodel, audio)
+    out["logits"] = logits.numpy()
+    out["tokens"] = logits.argmax(-1).numpy().astype(np.int32)
+    out["temporal_binding"] = feats["temporal_binding"].numpy()
+    out["fused_features"] = feats["fused_features"].numpy()
+    out["greedy"] = np.array(json.dumps(ref_decode.ctc_greedy_decode(logits)))
+    # the reference's own calibrate_model (quantize.py:325-369) on fresh QAT modules: eval-mode
+    # forwards pass through, then every quantizer is marked calibrated with scale 1, zp 0
+    from velocity_asr.quantize import calibrate_model, prepare_model_for_qat
+    torch.manual_seed(0)
+    m2 = prepare_model_for_qat(build_model())
+    sd2 = qat_state_from_fp32(m2, build_model().state_dict())
+    m2.load_state_dict(sd2, strict=True)
+    calibrate_model(m2, [(torch.from_numpy(np.zeros((1, 100, 80), np.float32)),)], num_batches=1, device="cpu")
+    with torch.no_grad():
+        lg2 = m2(mel)
+    out["refcal_logits"] = lg2.numpy()
+    out["modules"] = np.array(json.dumps(names))
+    # element-level known answers of FakeQuantize itself (bit-exact pins for the kernels)
+    from velocity_asr.quantize import FakeQuantize
+    rng = np.random.default_rng(72)
+    x = (rng.standard_normal((48, 40)) * 2.0).astype(np.float32)
+    x[0, :8] = [0.0, -0.0, 1e-12, -1e-12, 3.4e38, -3.4e38, 0.5, -0.5]
+    fq_cases = [("asym8", dict(bits=8, symmetric=False, per_channel=False)),
+                ("sym8_pc", dict(bits=8, symmetric=True, per_channel=True, channel_dim=0)),
+                ("sym8", dict(bits=8, symmetric=True, per_channel=False)),
+                ("asym4", dict(bits=4, symmetric=False, per_channel=False)),
+                ("sym6_pc", dict(bits=6, symmetric=True, per_channel=True, channel_dim=0))]
+    for name, kw in fq_cases:
+        fq = FakeQuantize(**kw).eval()
+        with torch.no_grad():
+            # per-tensor: calibrate on rows 1.. (row 0 holds extremes that then clamp)
+            fq.calibrate(torch.from_numpy(x if kw["per_channel"] else x[1:]))
+            y = fq(torch.from_numpy(x))
+        out[f"fq_{name}__y"] = y.numpy()
+        out[f"fq_{name}__scale"] = fq.scale.numpy()
+        out[f"fq_{name}__zp"] = fq.zero_point.numpy()
+    out["fq_x"] = x
+    out["fq_cases"] = np.array(json.dumps(fq_cases))
+    out["meta"] = meta(calib="make_audio(2, 48000, seed=71)", audio="make_audio(2, 48000, seed=21)",
+                       weights="make_weights(None, seed=0) carried into prepare_model_for_qat modules",
+                       batch=[2, 48000])
+    save("int8_b2_3s.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode"]
+    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8"]
     if "mel" in which:
         gen_mel()
     if "scan" in which:
@@ -318,3 +421,5 @@ if __name__ == "__main__":
         gen_forward_small_config()
     if "decode" in which:
         gen_decode()
+    if "int8" in which:
+        gen_int8()

@@ -30,6 +30,7 @@ struct GemmParams {
     int64_t ld_aux, stride_aux;
     const float* aux2;
     int n_out;
+    const float4* qp;  // per-column activation fake-quant {scale, zp, qmin, qmax} or null
 };
 
 struct Tile {
@@ -81,10 +82,16 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
             if (GUARD && col >= p.n_out) continue;
             const int pc = n0 + wc * 32 * TN + tp * 64 + r;  // paired column of half 0
             float bg = 0.f, bgl = 0.f, b2 = 0.f;
+            float4 qg, qgl, ql;
             if constexpr (EPI == VASR_EPI_PAIR_FUSION) {
                 bg = p.bias[pc];
                 bgl = p.bias[pc + 32];
                 b2 = p.aux2[col];
+                if (p.qp) {
+                    qg = p.qp[pc];
+                    qgl = p.qp[pc + 32];
+                    ql = p.qp[2 * p.n_out + col];
+                }
             }
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
@@ -100,9 +107,15 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
                     } else {
                         // aux: local-side partial products in the same paired layout.
                         const float* ar = auxb + (int64_t)row * p.ld_aux;
-                        const float gate = sigmoid_fast((ar[pc] + v0) + bg);
-                        const float lt = ar[pc + 32] + b2;
-                        const float gt = v1 + bgl;
+                        float gp = (ar[pc] + v0) + bg;
+                        float lt = ar[pc + 32] + b2;
+                        float gt = v1 + bgl;
+                        if (p.qp) {
+                            gp = fake_quant(gp, qg);
+                            lt = fake_quant(lt, ql);
+                            gt = fake_quant(gt, qgl);
+                        }
+                        const float gate = sigmoid_fast(gp);
                         out = gate * lt + (1.0f - gate) * gt;
                     }
                     Cb[(int64_t)row * p.ldc + col] = out;
@@ -117,6 +130,8 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
                 const int col = n0 + wc * 32 * TN + tn * 32 + r;
                 if (GUARD && col >= p.N) continue;
                 const float bv = p.bias ? p.bias[col] : 0.0f;
+                float4 qc;
+                if (p.qp) qc = p.qp[col];
                 // softplus columns: decided per 32-column MFMA tile (wave-uniform) where possible
                 const int cbase = n0 + wc * 32 * TN + tn * 32;
                 const bool sp_all = cbase >= p.n_out, sp_none = cbase + 32 <= p.n_out;
@@ -127,6 +142,7 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
                     if (GUARD && row >= p.M) continue;
                     float v = acc[tm][tn][i];
                     if (p.bias) v = v + bv;
+                    if (p.qp) v = fake_quant(v, qc);
                     if constexpr (EPI == VASR_EPI_GELU) {
                         v = gelu_fast(v);
                     } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
@@ -202,6 +218,8 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
         VASR_CHECK_ARG(a->aux != nullptr, "%s: epilogue %d needs aux", fn, epi);
     if (epi == VASR_EPI_PAIR_FUSION)
         VASR_CHECK_ARG(a->aux2 != nullptr && a->bias != nullptr, "%s: fusion needs bias and aux2", fn);
+    VASR_CHECK_ARG(!(a->qparams && epi == VASR_EPI_PAIR_POWER), "%s: qparams not allowed with PAIR_POWER", fn);
+    VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->qparams) & 15) == 0, "%s: qparams must be 16-byte aligned", fn);
     p.A = a->A; p.lda = a->lda; p.stride_a = a->stride_a;
     p.W = a->W; p.ldw = a->ldw; p.Wx = nullptr; p.Kp = 0;
     p.bias = a->bias;
@@ -209,6 +227,7 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
     p.M = a->M; p.N = a->N; p.K = a->K;
     p.aux = a->aux; p.ld_aux = a->ld_aux; p.stride_aux = a->stride_aux;
     p.aux2 = a->aux2; p.n_out = a->n_out;
+    p.qp = reinterpret_cast<const float4*>(a->qparams);
     return VASR_OK;
 }
 

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
     ln_row_to(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
 }
 
-constexpr int TT = 64;       // output rows per block
+constexpr int TT = 16;       // output rows per block (1024 blocks at B=32, L=501: 4 per CU)
 constexpr int kMaxC = 256;   // LDS row capacity
 constexpr int kMaxK = 8;
 

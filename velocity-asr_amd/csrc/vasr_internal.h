@@ -85,6 +85,22 @@ __device__ __forceinline__ float softplus20_fast(float x) {
 
 __device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + fast_exp(-x)); }
 
+// FakeQuantize._quantize/_dequantize + straight-through form (quantize.py:97, :118-133) with
+// every operation IEEE-rounded in torch's order: contraction is switched off for this block
+// (HIP compiles with -ffp-contract=fast, which would fuse (q - zp) * s into the following
+// subtraction and move results by an ulp); the division is the correctly rounded one.
+// q = {scale, zp, qmin, qmax}.  scale == 0 (never produced by calibration, which clamps it to
+// >= 1e-10) marks a column that is not quantized, so one parameter array can cover fused
+// quantized / plain outputs.
+__device__ __forceinline__ float fake_quant(float x, float4 q) {
+#pragma clang fp contract(off)
+    if (q.x == 0.0f) return x;
+    const float t = x / q.x + q.y;
+    const float r = fminf(fmaxf(__builtin_rintf(t), q.z), q.w);
+    const float xdq = (r - q.y) * q.x;
+    return x + (xdq - x);
+}
+
 }  // namespace vasr
 
 #define VASR_CHECK_ARG(cond, ...)            \

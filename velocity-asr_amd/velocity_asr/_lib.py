@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libvasr_hip.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "vasr.h"))
@@ -38,6 +38,7 @@ class GemmArgs(ctypes.Structure):
         ("aux", c_p), ("ld_aux", c_i64), ("stride_aux", c_i64),
         ("aux2", c_p),
         ("n_out", c_i32),
+        ("qparams", c_p),
     ]
 
 
@@ -60,6 +61,9 @@ _SIGNATURES = {
     "vasr_adaptive_pool_f32": ([c_p, c_p] + [ctypes.c_int] * 4 + [c_p], ctypes.c_int),
     "vasr_pooled_attention_f32": ([c_p, c_i64, c_p, c_p] + [ctypes.c_int] * 5 + [c_p], ctypes.c_int),
     "vasr_argmax_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
+    "vasr_fakequant_f32": ([c_p, c_i64, c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, ctypes.c_int, c_f32, c_f32,
+                            c_p], ctypes.c_int),
+    "vasr_minmax_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p], ctypes.c_int),
     "vasr_ctc_collapse": ([c_p] + [ctypes.c_int] * 4 + [c_p, c_p, c_p, c_p, c_p], ctypes.c_int),
 }
 

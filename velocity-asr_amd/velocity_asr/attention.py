@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib, ops
+from . import quantize as Q
 from ._prep import cached
 from .ssm import GlobalSSM
 
@@ -38,7 +39,9 @@ class AdaptivePool(nn.Module):
         B, L, D = x.shape
         pool_size = min(self._compute_pool_size(L, prev_pool_size), L)
         pooled = ops.adaptive_pool(x, pool_size)
-        out = ops.gemm(pooled.view(B * pool_size, D), self.pool_proj.weight, self.pool_proj.bias)
+        w, b, qp = Q.linear_parts(self.pool_proj)
+        out = ops.gemm(pooled.view(B * pool_size, D), w, b, qparams=qp)
+        Q.record(self.pool_proj, out)
         return out.view(B, pool_size, D), pool_size
 
 
@@ -63,10 +66,19 @@ class MultiHeadAttention(nn.Module):
         self.scale = math.sqrt(self.head_dim)
 
     def _kv_weights(self):
+        """[k_proj; v_proj] as one GEMM: weights, biases and (if either is quantized) the
+        per-column activation fake-quant of both halves."""
         def build():
-            return (torch.cat([self.k_proj.weight, self.v_proj.weight], 0).contiguous(),
-                    torch.cat([self.k_proj.bias, self.v_proj.bias], 0).contiguous())
-        return cached(self, "kv", (self.k_proj.weight, self.v_proj.weight, self.k_proj.bias, self.v_proj.bias), build)
+            A = self.attention_dim
+            w = torch.cat([Q.effective_weight(self.k_proj), Q.effective_weight(self.v_proj)], 0).contiguous()
+            b = torch.cat([Q.inner(self.k_proj).bias, Q.inner(self.v_proj).bias], 0).contiguous()
+            qk, qv = Q.act_qparams(self.k_proj, A), Q.act_qparams(self.v_proj, A)
+            qp = None
+            if qk is not None or qv is not None:
+                qp = torch.cat([Q.act_qparams_or_identity(self.k_proj, A, w.device),
+                                Q.act_qparams_or_identity(self.v_proj, A, w.device)], 0).contiguous()
+            return w, b, qp
+        return cached(self, "kv", Q.deps(self.k_proj) + Q.deps(self.v_proj), build)
 
     def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
                 mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -76,16 +88,24 @@ class MultiHeadAttention(nn.Module):
         B, Lq, D = query.shape
         Kp = key.shape[1]
         A = self.attention_dim
-        q = ops.gemm(query.reshape(B * Lq, D), self.q_proj.weight, self.q_proj.bias)
+        wq, bq, qpq = Q.linear_parts(self.q_proj)
+        q = ops.gemm(query.reshape(B * Lq, D), wq, bq, qparams=qpq)
+        Q.record(self.q_proj, q)
         if key is value:
-            w_kv, b_kv = self._kv_weights()
-            kv = ops.gemm(key.reshape(B * Kp, D), w_kv, b_kv)
+            w_kv, b_kv, qp_kv = self._kv_weights()
+            kv = ops.gemm(key.reshape(B * Kp, D), w_kv, b_kv, qparams=qp_kv)
         else:
             kv = torch.empty((B * Kp, 2 * A), device=query.device, dtype=torch.float32)
-            ops.gemm(key.reshape(B * Kp, D), self.k_proj.weight, self.k_proj.bias, out=kv[:, :A])
-            ops.gemm(value.reshape(B * Kp, D), self.v_proj.weight, self.v_proj.bias, out=kv[:, A:])
+            for mod, src, sl in ((self.k_proj, key, slice(0, A)), (self.v_proj, value, slice(A, 2 * A))):
+                w, b, qp = Q.linear_parts(mod)
+                ops.gemm(src.reshape(B * Kp, D), w, b, out=kv[:, sl], qparams=qp)
+        Q.record(self.k_proj, kv[:, :A])
+        Q.record(self.v_proj, kv[:, A:])
         o = ops.pooled_attention(q, kv, B, Lq, Kp, self.num_heads)
-        return ops.gemm(o, self.out_proj.weight, self.out_proj.bias).view(B, Lq, D)
+        wo, bo, qpo = Q.linear_parts(self.out_proj)
+        out = ops.gemm(o, wo, bo, qparams=qpo)
+        Q.record(self.out_proj, out)
+        return out.view(B, Lq, D)
 
 
 class GatedFusion(nn.Module):
@@ -99,32 +119,57 @@ class GatedFusion(nn.Module):
         self.out_proj = nn.Linear(d_model, d_model)
 
     def _paired(self):
-        """Rows interleaved in 32-row pairs so one wave holds gate and branch of the same column."""
+        """Rows interleaved in 32-row pairs so one wave holds gate and branch of the same column
+        (weights, biases and, for quantized layers, the epilogue's activation fake-quant)."""
+        gate, loc, glob = self.gate_proj[0], self.local_proj, self.global_proj
+
         def build():
-            D = self.local_proj.weight.shape[0]
+            D = Q.inner(loc).weight.shape[0]
             if D % 32:
                 raise NotImplementedError("GatedFusion on HIP needs d_model % 32 == 0")
-            Wg = self.gate_proj[0].weight
-            bg = self.gate_proj[0].bias
+            Wg = Q.effective_weight(gate)
+            bg = Q.inner(gate).bias
 
             def pair(a, b):
                 return torch.stack([a.reshape(D // 32, 32, *a.shape[1:]), b.reshape(D // 32, 32, *b.shape[1:])],
                                    1).reshape(2 * D, *a.shape[1:]).contiguous()
-            w_local = pair(Wg[:, :D], self.local_proj.weight)      # [gate_l | local_proj]
-            w_glob = pair(Wg[:, D:], self.global_proj.weight)      # [gate_g | global_proj]
-            b_glob = pair(bg, self.global_proj.bias)
-            return w_local, w_glob, b_glob
-        deps = (self.gate_proj[0].weight, self.gate_proj[0].bias, self.local_proj.weight, self.global_proj.weight,
-                self.global_proj.bias)
-        return cached(self, "paired", deps, build)
+            w_local = pair(Wg[:, :D], Q.effective_weight(loc))      # [gate_l | local_proj]
+            w_glob = pair(Wg[:, D:], Q.effective_weight(glob))      # [gate_g | global_proj]
+            b_glob = pair(bg, Q.inner(glob).bias)
+            qp = None
+            if any(Q.act_qparams(m, D) is not None for m in (gate, loc, glob)):
+                dev = Wg.device
+                qp = torch.cat([pair(Q.act_qparams_or_identity(gate, D, dev), Q.act_qparams_or_identity(glob, D, dev)),
+                                Q.act_qparams_or_identity(loc, D, dev)], 0).contiguous()
+            return w_local, w_glob, b_glob, qp
+        return cached(self, "paired", Q.deps(gate) + Q.deps(loc) + Q.deps(glob), build)
+
+    def _observe(self, local2: torch.Tensor, glob2: torch.Tensor) -> None:
+        """Calibration only: the raw (pre-quantizer) gate / local / global outputs, summed in
+        the fused epilogue's order ((local part + global part) + bias for the gate)."""
+        gate, loc, glob = self.gate_proj[0], self.local_proj, self.global_proj
+        D = local2.shape[1]
+        Wg = Q.effective_weight(gate)
+        if Q.observing(gate):
+            t = ops.gemm(local2, Wg[:, :D].contiguous())
+            Q.record(gate, ops.gemm(glob2, Wg[:, D:].contiguous(), epilogue=_lib.EPI_RESIDUAL, aux=t)
+                     + Q.inner(gate).bias.detach())
+        for mod, src in ((loc, local2), (glob, glob2)):
+            if Q.observing(mod):
+                Q.record(mod, ops.gemm(src, Q.effective_weight(mod), Q.inner(mod).bias))
 
     def forward(self, local_features: torch.Tensor, global_features: torch.Tensor) -> torch.Tensor:
         B, L, D = local_features.shape
-        w_local, w_glob, b_glob = self._paired()
-        t1 = ops.gemm(local_features.reshape(B * L, D), w_local)
-        fused = ops.gemm(global_features.reshape(B * L, D), w_glob, b_glob, epilogue=_lib.EPI_PAIR_FUSION, aux=t1,
-                         aux2=self.local_proj.bias, n_out=D)
-        return ops.gemm(fused, self.out_proj.weight, self.out_proj.bias).view(B, L, D)
+        local2, glob2 = local_features.reshape(B * L, D), global_features.reshape(B * L, D)
+        self._observe(local2, glob2)
+        w_local, w_glob, b_glob, qp = self._paired()
+        t1 = ops.gemm(local2, w_local)
+        fused = ops.gemm(glob2, w_glob, b_glob, epilogue=_lib.EPI_PAIR_FUSION, aux=t1,
+                         aux2=Q.inner(self.local_proj).bias, n_out=D, qparams=qp)
+        wo, bo, qpo = Q.linear_parts(self.out_proj)
+        out = ops.gemm(fused, wo, bo, qparams=qpo)
+        Q.record(self.out_proj, out)
+        return out.view(B, L, D)
 
 
 class HierarchicalGlobalContext(nn.Module):

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib, ops
+from . import quantize as Q
 from ._prep import cached
 from .attention import HierarchicalGlobalContext
 from .ssm import LocalSSMProcessor, ScanMode
@@ -94,26 +95,19 @@ class TemporalBindingLayer(nn.Module):
         self.norm = nn.LayerNorm(d_model)
         self.activation = nn.GELU()
 
-    def _w(self):
-        def build():
-            w = self.conv.weight  # (D, C, k) -> (D, k*C), frame-major like the im2col rows
-            return w.permute(0, 2, 1).reshape(w.shape[0], -1).contiguous()
-        return cached(self, "w", (self.conv.weight,), build)
-
     def output_length(self, frames: int) -> int:
-        k, s, p = self.conv.kernel_size[0], self.conv.stride[0], self.conv.padding[0]
+        c = Q.inner(self.conv)
+        k, s, p = c.kernel_size[0], c.stride[0], c.padding[0]
         return (frames + 2 * p - k) // s + 1
 
     def forward(self, mel_spectrogram: torch.Tensor) -> torch.Tensor:
-        B, F, C = mel_spectrogram.shape
-        k, s, p = self.conv.kernel_size[0], self.conv.stride[0], self.conv.padding[0]
-        D = self.conv.out_channels
-        L = self.output_length(F)
-        frames = max(F + 2 * p, (L - 1) * s + k)
-        buf = ops.pad_frames(mel_spectrogram, frames, p)
-        x = torch.empty((B, L, D), device=buf.device, dtype=torch.float32)
-        ops.gemm_batched(buf, s * C, frames * C, L, B, k * C, self._w(), self.conv.bias, x, D, L * D,
-                         epilogue=_lib.EPI_GELU_PE, aux=self.pos_encoding.table(L), ld_aux=D, stride_aux=0)
+        D = Q.inner(self.conv).out_channels
+        L = self.output_length(mel_spectrogram.shape[1])
+        if Q.observing(self.conv):
+            Q.record(self.conv, Q.conv1d_rows(self.conv, mel_spectrogram))
+        # conv (+ activation fake-quant for QuantizedConv1d) -> GELU -> + PE, one GEMM
+        x = Q.conv1d_rows(self.conv, mel_spectrogram, epilogue=_lib.EPI_GELU_PE, aux=self.pos_encoding.table(L),
+                          ld_aux=D)
         return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
 
 
@@ -126,9 +120,12 @@ class CTCOutputHead(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, L, D = x.shape
-        ln, lin = self.proj[0], self.proj[2]
+        ln = self.proj[0]
+        w, b, qp = Q.linear_parts(self.proj[2])
         h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
-        return ops.gemm(h.view(B * L, D), lin.weight, lin.bias).view(B, L, lin.out_features)
+        logits = ops.gemm(h.view(B * L, D), w, b, qparams=qp)
+        Q.record(self.proj[2], logits)
+        return logits.view(B, L, w.shape[0])
 
 
 class VELOCITYASR(nn.Module):

@@ -128,10 +128,21 @@ def _linear(args: GemmArgs, w: torch.Tensor, stream) -> None:
         check(L.lib().vasr_linear_f32(args, stream), "vasr_linear_f32")
 
 
+def _qp(qparams: Optional[torch.Tensor], cols: int) -> Optional[int]:
+    if qparams is None:
+        return None
+    _cuda_f32("gemm.qparams", qparams)
+    if not qparams.is_contiguous() or tuple(qparams.shape) != (cols, 4):
+        raise ValueError(f"gemm: qparams must be a contiguous ({cols}, 4) tensor, got {tuple(qparams.shape)}")
+    return qparams.data_ptr()
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, epilogue: int = L.EPI_NONE,
          out: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
-         aux2: Optional[torch.Tensor] = None, n_out: int = 0, n_cols_out: Optional[int] = None) -> torch.Tensor:
-    """out = epilogue(a @ w.T + bias) for a (M, K) row view and w (N, K)."""
+         aux2: Optional[torch.Tensor] = None, n_out: int = 0, n_cols_out: Optional[int] = None,
+         qparams: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = epilogue(fq(a @ w.T + bias)) for a (M, K) row view and w (N, K); fq is the
+    per-column activation fake-quant of `qparams` ((ncols, 4) {scale, zp, qmin, qmax}) if given."""
     _cuda_f32("gemm.a", a)
     _cuda_f32("gemm.w", w)
     M, K, lda = _rows("gemm.a", a)
@@ -154,6 +165,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
         args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, 0
     args.aux2 = ptr(aux2)
     args.n_out = n_out
+    args.qparams = _qp(qparams, N + (n_out if epilogue == L.EPI_PAIR_FUSION else 0))
     ev = _t0("gemm")
     _linear(args, w, stream_of(a))
     _t1("gemm", ev, dict(M=M, N=N, K=K, batch=1))
@@ -163,7 +175,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
 def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch: int, K: int, w: torch.Tensor,
                  bias: Optional[torch.Tensor], out: torch.Tensor, ldc: int, stride_c: int, *,
                  epilogue: int = L.EPI_NONE, aux: Optional[torch.Tensor] = None, ld_aux: int = 0,
-                 stride_aux: int = 0, n_out: int = 0) -> torch.Tensor:
+                 stride_aux: int = 0, n_out: int = 0, qparams: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Strided batched form: A[b] rows at a_base + b*stride_a + m*lda (overlapping rows allowed)."""
     _cuda_f32("gemm_batched.a", a_base)
     _cuda_f32("gemm_batched.w", w)
@@ -184,6 +196,7 @@ def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch
     if aux is not None:
         args.aux, args.ld_aux, args.stride_aux = aux.data_ptr(), ld_aux, stride_aux
     args.n_out = n_out
+    args.qparams = _qp(qparams, N)
     ev = _t0("gemm")
     _linear(args, w, stream_of(a_base))
     _t1("gemm", ev, dict(M=rows, N=N, K=K, batch=batch))
@@ -334,3 +347,53 @@ def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, time
     check(L.lib().vasr_ctc_collapse(pred.data_ptr(), B, Lq, int(blank), int(collapse), toks.data_ptr(),
                                     lens.data_ptr(), ptr(st), ptr(en), stream_of(pred)), "vasr_ctc_collapse")
     return toks, lens, st, en
+
+
+def fakequant(x: torch.Tensor, scale: torch.Tensor, zero_point: torch.Tensor, qmin: float, qmax: float,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """FakeQuantize (eval, calibrated) of x viewed as (dim0, rest): scale / zero_point hold
+    dim0 entries (per-channel, channel_dim 0) or one (per-tensor)."""
+    _cuda_f32("fakequant.x", x)
+    _cuda_f32("fakequant.scale", scale)
+    _cuda_f32("fakequant.zero_point", zero_point)
+    x = x.contiguous()
+    rows = x.shape[0] if x.dim() > 0 else 1
+    x2 = x.reshape(rows, -1)
+    cols = x2.shape[1]
+    n = scale.numel()
+    if zero_point.numel() != n or n not in (1, rows):
+        raise ValueError(f"fakequant: scale/zero_point of {n} entries for a tensor with {rows} channels")
+    y = torch.empty_like(x) if out is None else out
+    check(L.lib().vasr_fakequant_f32(x2.data_ptr(), cols, y.data_ptr(), cols, rows, cols,
+                                     scale.contiguous().data_ptr(), zero_point.contiguous().data_ptr(),
+                                     int(n == rows and n > 1), float(qmin), float(qmax), stream_of(x)),
+          "vasr_fakequant_f32")
+    return y
+
+
+def minmax(x: torch.Tensor, per_channel: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(min, max) over the whole tensor, or per channel of dim 0 (shape (dim0,))."""
+    _cuda_f32("minmax.x", x)
+    if x.numel() == 0:
+        raise RuntimeError("minmax: empty tensor")
+    x = x.contiguous()
+    if per_channel and x.dim() >= 1:
+        x2 = x.reshape(x.shape[0], -1)
+    else:
+        x2 = x.reshape(-1, x.shape[-1] if x.dim() >= 1 else 1)
+    rows, cols, ld = _rows("minmax.x", x2)
+    lo = torch.empty(rows, device=x.device, dtype=torch.float32)
+    hi = torch.empty(rows, device=x.device, dtype=torch.float32)
+    check(L.lib().vasr_minmax_f32(x2.data_ptr(), ld, rows, cols, lo.data_ptr(), hi.data_ptr(), stream_of(x)),
+          "vasr_minmax_f32")
+    if per_channel or rows == 1:
+        return lo, hi
+    lo1 = torch.empty(1, device=x.device, dtype=torch.float32)
+    hi1 = torch.empty(1, device=x.device, dtype=torch.float32)
+    lib = L.lib()
+    check(lib.vasr_minmax_f32(lo.data_ptr(), rows, 1, rows, lo1.data_ptr(), hi1.data_ptr(), stream_of(x)),
+          "vasr_minmax_f32")
+    scratch = torch.empty(1, device=x.device, dtype=torch.float32)
+    check(lib.vasr_minmax_f32(hi.data_ptr(), rows, 1, rows, scratch.data_ptr(), hi1.data_ptr(), stream_of(x)),
+          "vasr_minmax_f32")
+    return lo1, hi1
