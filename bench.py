@@ -121,6 +121,8 @@ def main():
     ap.add_argument("--streams", type=int, default=1, help="utterance groups replayed on concurrent HIP streams")
     ap.add_argument("--int8", action="store_true",
                     help="BASELINE configs[4]: INT8 fake-quant model (prepare_model_for_qat + activation calibration)")
+    ap.add_argument("--bf16", action="store_true",
+                    help="BASELINE configs[2] per-GPU shape: the model as bf16 (bf16 weights / MFMA operands)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -135,6 +137,8 @@ def main():
     from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids
 
     model = build_model(dev)
+    if args.bf16:
+        model = model.to(torch.bfloat16)
     if args.int8:
         from velocity_asr import compute_mel_spectrogram
         from velocity_asr import quantize as Q
@@ -221,10 +225,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if args.bf16 else "f32",
         "data": "synthetic: N(0, 0.1) 16 kHz clips; seeded random-init weights (velocity_asr.synthetic)",
         "config": {"workload": f"{B} x {args.seconds:g} s clips per GPU, audio->mel->forward->CTC greedy tokens "
-                               f"(BASELINE configs[{4 if args.int8 else 1}]"
+                               f"(BASELINE configs[{4 if args.int8 else 2 if args.bf16 else 1}]"
                                f"{', INT8 fake-quant' if args.int8 else ''}"
                                f"{f', HIP graph x{args.streams} streams' if not args.eager else ', eager'})",
                    "global_batch": world * B, "clip_seconds": args.seconds, "parallelism": f"utterance-shard x{world}"},

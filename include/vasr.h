@@ -103,6 +103,17 @@ int vasr_linear_x3_f32(const vasr_gemm_args* args, const uint16_t* w_split, void
 int vasr_split_weights_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
 int64_t vasr_split_weights_elems(int N, int K);
 
+/* The GEMM of a bf16 model (BASELINE config C3, `model.to(torch.bfloat16)`): W is bf16,
+ * packed once by vasr_pack_weights_bf16 into the same fragment-native layout with one plane
+ * (out[NT][KS][64][8], vasr_pack_weights_bf16_elems(N, K) = 32*NT * Kp elements); A stays
+ * fp32 in HBM and is rounded to bf16 (round-to-nearest-even) as it enters the MFMA
+ * (v_mfma_f32_32x32x16_bf16), accumulation and epilogues in fp32 — the reference's bf16
+ * Linear (ssm.py, attention.py, model.py nn.Linear under bf16 parameters) with fp32
+ * accumulation.  Same args and epilogues as vasr_linear_f32. */
+int vasr_linear_bf16(const vasr_gemm_args* args, const uint16_t* w_packed, void* stream);
+int vasr_pack_weights_bf16(const uint16_t* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
+int64_t vasr_pack_weights_bf16_elems(int N, int K);
+
 /* ------------------------------------------------------------------ norms / conv
  * nn.LayerNorm over the last dim (C <= 1024), biased variance.  y may alias x.
  * Replaces every LayerNorm on the path (26 per forward).

@@ -407,8 +407,28 @@ def gen_int8():
     save("int8_b2_3s.npz", **out)
 
 
+# --------------------------------------------------------------------------- bf16 (C3)
+def gen_bf16():
+    """The reference run as a bf16 model: model.to(torch.bfloat16), fp32 audio -> mel, mel cast
+    to bf16 (every op of the forward then computes in bf16 on the CPU)."""
+    model = build_model().to(torch.bfloat16)
+    out = {}
+    for name, (B, S, seed) in {"b2_3s": (2, 48000, 21), "b2_10s": (2, 160000, 1234)}.items():
+        audio = syn.make_audio(B, S, seed=seed)
+        with torch.no_grad():
+            mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(audio))
+            logits = model(mel.to(torch.bfloat16)).float()
+        out[name + ("__logits" if S < 100000 else "__logits_sub10")] = (logits.numpy() if S < 100000
+                                                                          else logits[:, ::10].numpy())
+        out[name + "__tokens"] = logits.argmax(-1).numpy().astype(np.int32)
+        out[name + "__greedy"] = np.array(json.dumps(ref_decode.ctc_greedy_decode(logits)))
+    out["meta"] = meta(weights="make_weights(None, seed=0) -> model.to(bfloat16)",
+                       audio="b2_3s: make_audio(2, 48000, seed=21); b2_10s: make_audio(2, 160000, seed=1234)")
+    save("bf16_fwd.npz", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8"]
+    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8", "bf16"]
     if "mel" in which:
         gen_mel()
     if "scan" in which:
@@ -423,3 +443,5 @@ if __name__ == "__main__":
         gen_decode()
     if "int8" in which:
         gen_int8()
+    if "bf16" in which:
+        gen_bf16()

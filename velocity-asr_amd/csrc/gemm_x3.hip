@@ -88,14 +88,18 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int WM, int WN, int TM, int TN, int RING, int EPI>
-__global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <= 81920 ? 2 : 1) void gemm_x3_kernel(GemmParams p) {
+// P = 3: the split-bf16 fp32 GEMM described above.  P = 1: the bf16 GEMM of a bf16 model
+// (vasr_linear_bf16): W is one bf16 plane, A is rounded to bf16 (RNE) at the fragment read,
+// one MFMA per k-step, fp32 accumulation — same staging, same epilogues.
+template <int WM, int WN, int TM, int TN, int RING, int EPI, int P>
+__global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 2048 * P) <= 81920 ? 2 : 1) void gemm_x3_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
     static_assert(WM * WN == 4, "4 waves");
+    static_assert(P == 1 || P == 3, "planes");
     static_assert(TN % 2 == 0 || (EPI != VASR_EPI_PAIR_POWER && EPI != VASR_EPI_PAIR_FUSION), "pairs need even TN");
     constexpr int A_BYTES = BM * BK * 4;            // fp32 [BM][32]
-    constexpr int W_BYTES = (BN / 32) * 6 * 1024;   // [BN/32][2 k-steps][3 planes][64][16 B]
+    constexpr int W_BYTES = (BN / 32) * 2 * P * 1024;  // [BN/32][2 k-steps][P planes][64][16 B]
     constexpr int A_INSTR = A_BYTES / 1024, W_INSTR = W_BYTES / 1024;
     static_assert(A_INSTR % 4 == 0 && W_INSTR % 4 == 0, "whole LDS-DMA pieces per wave");
 
@@ -159,9 +163,9 @@ __global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <
 #pragma unroll
         for (int jj = 0; jj < W_INSTR / 4; ++jj) {
             const int j = jj * 4 + wave_u;
-            const int tnl = j / 6, rem = j - tnl * 6;  // rem = k-step * 3 + plane
+            const int tnl = j / (2 * P), rem = j - tnl * (2 * P);  // rem = k-step * P + plane
             const int nt = min(n0 / 32 + tnl, NT - 1);
-            const char* src = Wf + ((int64_t)(nt * KS + 2 * kt) * 3 + rem) * 1024 + lane * 16;
+            const char* src = Wf + ((int64_t)(nt * KS + 2 * kt) * P + rem) * 1024 + lane * 16;
             glds16(src, wbuf + j * 1024);
         }
     };
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <
     // work the scheduler places in the shadow of step 0's MFMAs.
     auto compute = [&](const char* abuf, const char* wbuf) {
         float4 xa[2][TM][2];
-        bf16x8 fw[2][3][TN];
+        bf16x8 fw[2][P][TN];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int c0 = 4 * s + 2 * h;
@@ -193,23 +197,28 @@ __global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
+                for (int pl = 0; pl < P; ++pl)
                     fw[s][pl][tn] = *reinterpret_cast<const bf16x8*>(
-                        wbuf + (((wc * TN + tn) * 2 + s) * 3 + pl) * 1024 + lane * 16);
+                        wbuf + (((wc * TN + tn) * 2 + s) * P + pl) * 1024 + lane * 16);
         }
-        bf16x8 fa[2][3][TM];
+        bf16x8 fa[2][P][TM];
         auto split_step = [&](int s) {
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
-                if constexpr (VASR_X3_ABLATE & 4) {
+                if constexpr (P == 1) {
                     const float4 x0 = xa[s][tm][0], x1 = xa[s][tm][1];
                     const bf16x8 v = {(__bf16)x0.x, (__bf16)x0.y, (__bf16)x0.z, (__bf16)x0.w,
                                       (__bf16)x1.x, (__bf16)x1.y, (__bf16)x1.z, (__bf16)x1.w};
                     fa[s][0][tm] = v;
-                    fa[s][1][tm] = v;
-                    fa[s][2][tm] = v;
+                } else if constexpr (VASR_X3_ABLATE & 4) {
+                    const float4 x0 = xa[s][tm][0], x1 = xa[s][tm][1];
+                    const bf16x8 v = {(__bf16)x0.x, (__bf16)x0.y, (__bf16)x0.z, (__bf16)x0.w,
+                                      (__bf16)x1.x, (__bf16)x1.y, (__bf16)x1.z, (__bf16)x1.w};
+                    fa[s][0][tm] = v;
+                    fa[s][P - 1][tm] = v;
+                    fa[s][P / 2][tm] = v;
                 } else {
-                    split8(xa[s][tm][0], xa[s][tm][1], fa[s][0][tm], fa[s][1][tm], fa[s][2][tm]);
+                    split8(xa[s][tm][0], xa[s][tm][1], fa[s][0][tm], fa[s][P / 2][tm], fa[s][P - 1][tm]);
                 }
             }
         };
@@ -218,9 +227,18 @@ __global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <
 #pragma unroll
                 for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)fa[s][0][tm][0] * (float)fw[s][2][tn][1];
+                    for (int tn = 0; tn < TN; ++tn) acc[tm][tn][0] += (float)fa[s][0][tm][0] * (float)fw[s][P - 1][tn][1];
                 return;
             }
+            if constexpr (P == 1) {
+#pragma unroll
+                for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+                    for (int tn = 0; tn < TN; ++tn)
+                        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][tm], fw[s][0][tn], acc[tm][tn],
+                                                                              0, 0, 0);
+                return;
+            } else {
             // small terms first, then the leading hi*hi term
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm)
@@ -235,6 +253,7 @@ __global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <
                     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][0][tm], fw[s][0][tn], c, 0, 0, 0);
                     acc[tm][tn] = c;
                 }
+            }
         };
         split_step(0);
         mfma_step(0);
@@ -300,14 +319,14 @@ __global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 6144) <
     epilogue<BM, BN, TM, TN, EPI>(p, t, acc, wr, wc, r, h);
 }
 
-template <int WM, int WN, int TM, int TN, int RING>
+template <int WM, int WN, int TM, int TN, int RING, int P>
 int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
     const int tiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
     dim3 grid(tiles, batch);
     dim3 block(256);
-#define VASR_L(E) hipLaunchKernelGGL((gemm_x3_kernel<WM, WN, TM, TN, RING, E>), grid, block, 0, s, p)
+#define VASR_L(E) hipLaunchKernelGGL((gemm_x3_kernel<WM, WN, TM, TN, RING, E, P>), grid, block, 0, s, p)
     switch (epi) {
         case VASR_EPI_NONE: VASR_L(VASR_EPI_NONE); break;
         case VASR_EPI_GELU: VASR_L(VASR_EPI_GELU); break;
@@ -379,6 +398,24 @@ __global__ void split_weights_kernel(const float* __restrict__ W, int64_t ldw, i
     *reinterpret_cast<bf16x8*>(out + base + 1024) = lo;
 }
 
+// One bf16 plane in the same fragment-native layout [NT][KS][64][8] from a bf16 (N, K) matrix.
+__global__ void pack_bf16_kernel(const uint16_t* __restrict__ W, int64_t ldw, int N, int K, int Kp,
+                                 uint16_t* __restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int cpr = Kp / 8;
+    const int NT = (N + 31) / 32;
+    if (q >= (int64_t)NT * 32 * cpr) return;
+    const int n = (int)(q / cpr), k0 = (int)(q % cpr) * 8;
+    uint16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (n < N && k0 + j < K) ? W[(int64_t)n * ldw + k0 + j] : (uint16_t)0;
+    const int KS = Kp / 16;
+    const int lane = 32 * ((k0 % 16) / 8) + n % 32;
+    uint16_t* dst = out + ((int64_t)(n / 32) * KS + k0 / 16) * 512 + lane * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j] = v[j];
+}
+
 }  // namespace
 }  // namespace vasr
 
@@ -418,8 +455,45 @@ VASR_API int vasr_linear_x3_f32(const vasr_gemm_args* a, const uint16_t* w_split
     const int cfg = pick_x3(a->M, a->N, a->batch, pair);
 #endif
     switch (cfg) {
-        case 0: return launch_cfg<2, 2, 2, 2, RING_BIG>(p, a->batch, epi, s);
-        case 1: return launch_cfg<4, 1, 1, 2, RING_BIG>(p, a->batch, epi, s);
-        default: return launch_cfg<2, 2, 1, 1, RING_SMALL>(p, a->batch, epi, s);
+        case 0: return launch_cfg<2, 2, 2, 2, RING_BIG, 3>(p, a->batch, epi, s);
+        case 1: return launch_cfg<4, 1, 1, 2, RING_BIG, 3>(p, a->batch, epi, s);
+        default: return launch_cfg<2, 2, 1, 1, RING_SMALL, 3>(p, a->batch, epi, s);
+    }
+}
+
+VASR_API int64_t vasr_pack_weights_bf16_elems(int N, int K) {
+    if (N <= 0 || K <= 0) return 0;
+    return (int64_t)((N + 31) / 32 * 32) * ((K + 31) / 32 * 32);
+}
+
+VASR_API int vasr_pack_weights_bf16(const uint16_t* W, int64_t ldw, int N, int K, uint16_t* out, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(W && out, "vasr_pack_weights_bf16: null pointer");
+    VASR_CHECK_ARG(N > 0 && K > 0 && ldw >= K, "vasr_pack_weights_bf16: bad shape N=%d K=%d ldw=%lld", N, K,
+                   (long long)ldw);
+    VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "vasr_pack_weights_bf16: out must be 16-byte aligned");
+    const int Kp = (K + 31) / 32 * 32;
+    const int64_t n = (int64_t)((N + 31) / 32 * 32) * (Kp / 8);
+    hipLaunchKernelGGL(pack_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), W, ldw, N,
+                       K, Kp, out);
+    return launch_status("vasr_pack_weights_bf16");
+}
+
+VASR_API int vasr_linear_bf16(const vasr_gemm_args* a, const uint16_t* w_packed, void* stream) {
+    using namespace vasr;
+    GemmParams p;
+    if (int rc = check_args(a, "vasr_linear_bf16", p)) return rc;
+    VASR_CHECK_ARG(w_packed != nullptr && (reinterpret_cast<uintptr_t>(w_packed) & 15) == 0,
+                   "vasr_linear_bf16: w_packed must be a 16-byte aligned device pointer");
+    if (a->M == 0) return VASR_OK;
+    p.Wx = w_packed;
+    p.Kp = (a->K + 31) / 32 * 32;
+    const int epi = a->epilogue;
+    const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
+    hipStream_t s = as_stream(stream);
+    switch (pick_x3(a->M, a->N, a->batch, pair)) {
+        case 0: return launch_cfg<2, 2, 2, 2, RING_BIG, 1>(p, a->batch, epi, s);
+        case 1: return launch_cfg<4, 1, 1, 2, RING_BIG, 1>(p, a->batch, epi, s);
+        default: return launch_cfg<2, 2, 1, 1, RING_SMALL, 1>(p, a->batch, epi, s);
     }
 }

@@ -49,6 +49,9 @@ _SIGNATURES = {
     "vasr_linear_x3_f32": ([ctypes.POINTER(GemmArgs), c_p, c_p], ctypes.c_int),
     "vasr_split_weights_bf16x3": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
     "vasr_split_weights_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
+    "vasr_linear_bf16": ([ctypes.POINTER(GemmArgs), c_p, c_p], ctypes.c_int),
+    "vasr_pack_weights_bf16": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
+    "vasr_pack_weights_bf16_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_layer_norm_f32": ([c_p, c_i64, c_p, c_p, c_p, c_i64, ctypes.c_int, ctypes.c_int, c_f32, c_p], ctypes.c_int),
     "vasr_add_table_f32": ([c_p, c_p, c_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_p], ctypes.c_int),
     "vasr_ln_dwconv_f32": ([c_p, c_p, c_p, c_p, c_p, c_p] + [ctypes.c_int] * 4 + [c_f32, c_p], ctypes.c_int),

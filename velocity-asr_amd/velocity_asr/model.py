@@ -71,7 +71,7 @@ class PositionalEncoding2D(nn.Module):
         def build():
             half = self.pe_time.shape[1]
             return torch.cat([self.pe_time[:seq_len], self.pe_freq.reshape(1, half).expand(seq_len, half)],
-                             -1).contiguous()
+                             -1).float().contiguous()
         return cached(self, f"pe{seq_len}", (self.pe_time, self.pe_freq), build)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

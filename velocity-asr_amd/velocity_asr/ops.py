@@ -71,6 +71,33 @@ def _cuda_f32(name: str, t: torch.Tensor) -> None:
         raise TypeError(f"{name}: expected float32, got {t.dtype}")
 
 
+def _cuda_w(name: str, t: torch.Tensor) -> None:
+    """GEMM weights: float32 (fp32 GEMM) or bfloat16 (bf16 model, vasr_linear_bf16)."""
+    if isinstance(t, torch.Tensor) and t.dtype == torch.bfloat16 and t.device.type == "cuda":
+        return
+    _cuda_f32(name, t)
+
+
+# fp32 copies of bf16 parameters for the kernels that take fp32 operands (norm weights, biases,
+# conv taps, D, tables): built once per (tensor, version), dropped with the tensor.
+_f32_copies = {}
+
+
+def f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """t itself if float32 (or None), else a cached float32 copy (bf16 models)."""
+    if t is None or t.dtype == torch.float32:
+        return t
+    sig = (t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()))
+    ent = _f32_copies.get(id(t))
+    if ent is not None and ent[0]() is t and ent[1] == sig:
+        return ent[2]
+    with torch.no_grad():
+        c = t.detach().float().contiguous()
+    key = id(t)
+    _f32_copies[key] = (weakref.ref(t, lambda _r, k=key: _f32_copies.pop(k, None)), sig, c)
+    return c
+
+
 def _rows(name: str, t: torch.Tensor) -> Tuple[int, int, int]:
     """(rows, cols, row_stride) of a 2-D row-major view with unit column stride."""
     if t.dim() != 2:
@@ -121,8 +148,25 @@ def split_weights(w: torch.Tensor) -> torch.Tensor:
     return planes
 
 
+def pack_bf16(w: torch.Tensor) -> torch.Tensor:
+    """One fragment-native bf16 plane (as int16 storage) of a (N, K) bf16 weight view."""
+    N, K, ldw = _rows("pack.w", w)
+    sig = (w.data_ptr(), w._version, N, K, ldw)
+    ent = _splits.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == sig:
+        return ent[2]
+    packed = torch.empty(int(L.lib().vasr_pack_weights_bf16_elems(N, K)), device=w.device, dtype=torch.int16)
+    check(L.lib().vasr_pack_weights_bf16(w.data_ptr(), ldw, N, K, packed.data_ptr(), stream_of(w)),
+          "vasr_pack_weights_bf16")
+    key = id(w)
+    _splits[key] = (weakref.ref(w, lambda _r, k=key: _splits.pop(k, None)), sig, packed)
+    return packed
+
+
 def _linear(args: GemmArgs, w: torch.Tensor, stream) -> None:
-    if _gemm_mode == "x3":
+    if w.dtype == torch.bfloat16:
+        check(L.lib().vasr_linear_bf16(args, pack_bf16(w).data_ptr(), stream), "vasr_linear_bf16")
+    elif _gemm_mode == "x3":
         check(L.lib().vasr_linear_x3_f32(args, split_weights(w).data_ptr(), stream), "vasr_linear_x3_f32")
     else:
         check(L.lib().vasr_linear_f32(args, stream), "vasr_linear_f32")
@@ -144,7 +188,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     """out = epilogue(fq(a @ w.T + bias)) for a (M, K) row view and w (N, K); fq is the
     per-column activation fake-quant of `qparams` ((ncols, 4) {scale, zp, qmin, qmax}) if given."""
     _cuda_f32("gemm.a", a)
-    _cuda_f32("gemm.w", w)
+    _cuda_w("gemm.w", w)
+    bias, aux, aux2 = f32(bias), f32(aux), f32(aux2)
     M, K, lda = _rows("gemm.a", a)
     N, Kw, ldw = _rows("gemm.w", w)
     if Kw != K:
@@ -178,7 +223,8 @@ def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch
                  stride_aux: int = 0, n_out: int = 0, qparams: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Strided batched form: A[b] rows at a_base + b*stride_a + m*lda (overlapping rows allowed)."""
     _cuda_f32("gemm_batched.a", a_base)
-    _cuda_f32("gemm_batched.w", w)
+    _cuda_w("gemm_batched.w", w)
+    bias, aux = f32(bias), f32(aux)
     need = (batch - 1) * stride_a + (rows - 1) * lda + K
     avail = a_base.untyped_storage().nbytes() // 4 - a_base.storage_offset()
     if rows > 0 and batch > 0 and need > avail:
@@ -206,6 +252,7 @@ def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch
 def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _cuda_f32("layer_norm.x", x)
+    w, b = f32(w), f32(b)
     C = x.shape[-1]
     x2 = x.reshape(-1, C)
     rows, _, ldx = _rows("layer_norm.x", x2)
@@ -219,6 +266,7 @@ def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1
 def add_table(x: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     """x (B, L, C) + table (L, C) broadcast over the batch."""
     _cuda_f32("add_table.x", x)
+    table = f32(table)
     _cuda_f32("add_table.table", table)
     x = x.contiguous()
     B, Lq, C = x.shape
@@ -233,6 +281,7 @@ def add_table(x: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
 def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) -> torch.Tensor:
     """(B, L, C) -> causal depthwise conv of LayerNorm(x)."""
     _cuda_f32("ln_dwconv.x", x)
+    ln_w, ln_b, conv_w, conv_b = f32(ln_w), f32(ln_b), f32(conv_w), f32(conv_b)
     x = x.contiguous()
     B, Lq, C = x.shape
     Kc = conv_w.shape[-1]
@@ -246,6 +295,7 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
 def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Tensor, D: torch.Tensor, B: int,
              Lq: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gated selective scan.  xz (B*L, 2Di) [x|z], dt (B*L, Di), bc (B*L, 2N) [B|C] (row views)."""
+    D = f32(D)
     for n, t in (("xz", xz), ("dt", dt), ("bc", bc), ("A2", A2), ("D", D)):
         _cuda_f32(f"ssm_scan.{n}", t)
     M, two_di, ld_xz = _rows("ssm_scan.xz", xz)

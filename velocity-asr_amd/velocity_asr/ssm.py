@@ -68,7 +68,7 @@ class SelectiveSSM(nn.Module):
         def build():
             dev = self.x_proj.weight.device
             w = torch.cat([self.x_proj.weight, self.dt_proj.weight], 0).contiguous()
-            b = torch.cat([torch.zeros(2 * self.state_dim, device=dev), self.dt_proj.bias]).contiguous()
+            b = torch.cat([torch.zeros(2 * self.state_dim, device=dev), self.dt_proj.bias.float()]).contiguous()
             # A = -exp(A_log) exactly as the reference evaluates it (float32, ssm.py:116), then
             # pre-scaled by log2(e) so the kernel's dA is one v_exp_f32.
             A = -torch.exp(self.A_log.detach().float().cpu())
@@ -118,8 +118,8 @@ class SSMBlock(nn.Module):
         _check_eval(self)
         B, L, D = x.shape
         x = x.contiguous()
-        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, self.conv.weight.view(D, -1), self.conv.bias,
-                          self.norm1.eps)
+        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
+                          self.conv.bias, self.norm1.eps)
         g = self.ssm.gated_scan(u.view(B * L, D), B, L)
         x2 = x.view(B * L, D)
         x1 = ops.gemm(g, self.ssm.out_proj.weight, epilogue=_lib.EPI_RESIDUAL, aux=x2)
