@@ -22,13 +22,14 @@ SHAPES = [  # name, M, N, K, lda, epilogue, n_out
 
 
 def main():
-    for mode in (sys.argv[1:] or ["x3", "f32"]):
-        ops.set_gemm_mode(mode)
+    for mode in (sys.argv[1:] or ["x3", "f32", "bf16"]):
+        if mode != "bf16":
+            ops.set_gemm_mode(mode)
         print(f"--- {mode}")
-        run()
+        run(bf16=mode == "bf16")
 
 
-def run():
+def run(bf16=False):
     reps = int(os.environ.get("GEMM_REPS", "30"))
     only = os.environ.get("GEMM_SHAPES")
     tot = 0.0
@@ -37,6 +38,8 @@ def run():
             continue
         a = torch.randn(m, lda, device="cuda")[:, :k]
         w = torch.randn(n, k, device="cuda") * 0.05
+        if bf16:
+            w = w.to(torch.bfloat16)
         b = torch.randn(n, device="cuda")
         aux = torch.randn(m, n, device="cuda") if epi == _lib.EPI_RESIDUAL else None
         out = torch.empty(m, n, device="cuda")

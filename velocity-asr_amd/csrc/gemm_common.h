@@ -31,6 +31,7 @@ struct GemmParams {
     const float* aux2;
     int n_out;
     const float4* qp;  // per-column activation fake-quant {scale, zp, qmin, qmax} or null
+    int batch;
 };
 
 struct Tile {
@@ -170,6 +171,8 @@ __device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, flo
         epilogue_body<TM, TN, EPI, true>(p, t, acc, wr, wc, r, h);
 }
 
+
+
 // Tile configurations: {WM, WN, TM, TN, blocks per CU the kernel's VGPR/LDS use admits}.
 struct TileCfg {
     int wm, wn, tm, tn, occ;
@@ -228,6 +231,7 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
     p.aux = a->aux; p.ld_aux = a->ld_aux; p.stride_aux = a->stride_aux;
     p.aux2 = a->aux2; p.n_out = a->n_out;
     p.qp = reinterpret_cast<const float4*>(a->qparams);
+    p.batch = a->batch;
     return VASR_OK;
 }
 

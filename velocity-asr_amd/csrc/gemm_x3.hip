@@ -91,8 +91,20 @@ __device__ __forceinline__ void wait_vmcnt() {
 // P = 3: the split-bf16 fp32 GEMM described above.  P = 1: the bf16 GEMM of a bf16 model
 // (vasr_linear_bf16): W is one bf16 plane, A is rounded to bf16 (RNE) at the fragment read,
 // one MFMA per k-step, fp32 accumulation — same staging, same epilogues.
+// Blocks per CU the register allocation targets: as many as the LDS ring admits (<= 160 KiB).
+template <int WM, int WN, int TM, int TN, int RING, int P>
+constexpr int x3_occ() {
+    constexpr int lds = RING * (WM * 32 * TM * 128 + WN * TN * 2048 * P);
+#ifdef VASR_GEMM_OCC_CAP
+    constexpr int cap = VASR_GEMM_OCC_CAP;
+#else
+    constexpr int cap = 2;
+#endif
+    return 163840 / lds >= cap ? cap : (163840 / lds >= 1 ? 163840 / lds : 1);
+}
+
 template <int WM, int WN, int TM, int TN, int RING, int EPI, int P>
-__global__ __launch_bounds__(256, RING * (WM * 32 * TM * 128 + WN * TN * 2048 * P) <= 81920 ? 2 : 1) void gemm_x3_kernel(GemmParams p) {
+__global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm_x3_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
     static_assert(WM * WN == 4, "4 waves");
@@ -345,6 +357,7 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     return launch_status("vasr_linear_x3_f32");
 }
 
+
 // Tile shapes, largest first.  Measured (tools/gemm_variant_sweep.py, M = 16032): the
 // 128 x 128 tile has the best main loop (1.0 : 0.89 for 128 x 64 : 0.76 for 64 x 64 at long K)
 // and wins whenever it still yields about two tiles per CU; below that the CU balance of the
@@ -354,6 +367,10 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
 #endif
 constexpr int RING_SMALL = VASR_X3_RING;                      // 64 x 64 tiles
 constexpr int RING_BIG = VASR_X3_RING > 3 ? 3 : VASR_X3_RING;  // larger tiles
+#ifndef VASR_BF16_RING
+#define VASR_BF16_RING 2
+#endif
+constexpr int RING_B16 = VASR_BF16_RING;  // bf16 (one plane): a stage is 24 KiB at 128 x 128
 constexpr TileCfg kCfgs[] = {
     {2, 2, 2, 2, 2},  // 128 x 128
     {4, 1, 1, 2, 2},  // 128 x  64
@@ -491,9 +508,14 @@ VASR_API int vasr_linear_bf16(const vasr_gemm_args* a, const uint16_t* w_packed,
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     hipStream_t s = as_stream(stream);
-    switch (pick_x3(a->M, a->N, a->batch, pair)) {
-        case 0: return launch_cfg<2, 2, 2, 2, RING_BIG, 1>(p, a->batch, epi, s);
-        case 1: return launch_cfg<4, 1, 1, 2, RING_BIG, 1>(p, a->batch, epi, s);
-        default: return launch_cfg<2, 2, 1, 1, RING_SMALL, 1>(p, a->batch, epi, s);
+#ifdef VASR_BF16_FORCE_CFG
+    const int cfg = VASR_BF16_FORCE_CFG;  // diagnostic builds only
+#else
+    const int cfg = pick_x3(a->M, a->N, a->batch, pair);
+#endif
+    switch (cfg) {
+        case 0: return launch_cfg<2, 2, 2, 2, RING_B16, 1>(p, a->batch, epi, s);
+        case 1: return launch_cfg<4, 1, 1, 2, RING_B16, 1>(p, a->batch, epi, s);
+        default: return launch_cfg<2, 2, 1, 1, RING_B16, 1>(p, a->batch, epi, s);
     }
 }
