@@ -1,0 +1,87 @@
+"""CTC head with the row argmax fused into the GEMM epilogue (SURVEY §8 f rank 1): the
+(B, L, V) logits are never written.  Integer output, so the bar is bit-exact: the fused
+argmax must equal torch's argmax (first index on ties, decode.py:46) of the logits the same
+GEMM engine writes, and the reference goldens' tokens."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_json
+from oracle import velocity_ref as R
+from velocity_asr import synthetic as S
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def va():
+    import velocity_asr
+    from velocity_asr import _lib
+    _lib.require_device()
+    _lib.load()
+    return velocity_asr
+
+
+@pytest.mark.parametrize("engine", ["x3", "f32", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(1, 64, 32), (77, 1000, 192), (16032, 1000, 192), (300, 50, 96), (129, 257, 192)])
+def test_gemm_argmax_matches_logits(va, engine, M, N, K):
+    from velocity_asr import ops
+    g = torch.Generator().manual_seed(M + N)
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    w[N // 2] = w[N // 3]             # duplicate rows -> exact ties between two columns
+    w[N - 1] = w[N // 3]
+    b = torch.randn(N, generator=g) * 0.1
+    b[N // 2] = b[N // 3]
+    b[N - 1] = b[N // 3]
+    a[: M // 2] *= 0.0                # rows whose logits are the bias alone (ties on bias)
+    if engine == "bf16":
+        w = w.to(torch.bfloat16)
+    prev = ops.set_gemm_mode("x3" if engine == "bf16" else engine)
+    try:
+        A, W, Bv = a.to(DEV), w.to(DEV), b.to(DEV)
+        logits = ops.gemm(A, W, Bv)
+        want = torch.argmax(logits, dim=-1).to(torch.int32).cpu()
+        got = ops.gemm_argmax(A, W, Bv).cpu()
+    finally:
+        ops.set_gemm_mode(prev)
+    assert torch.equal(got, want)
+
+
+def test_model_token_ids(va):
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    for fname, (B, S_, seed) in (("fwd_b2_10s.npz", (2, 160000, 1234)), ("fwd_b2_3s.npz", (2, 48000, 21))):
+        audio = torch.from_numpy(S.make_audio(B, S_, seed=seed)).to(DEV)
+        mel = va.compute_mel_spectrogram(audio)
+        ids = m.token_ids(mel).cpu().numpy()
+        logits = m(mel)
+        assert np.array_equal(ids, logits.argmax(-1).cpu().numpy())
+        assert np.array_equal(ids, golden(fname)["tokens"])
+
+
+def test_pipeline_tokens_equal_golden_greedy(va):
+    from velocity_asr.pipeline import audio_to_token_ids, token_lists
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    audio = torch.from_numpy(S.make_audio(2, 160000, seed=1234)).to(DEV)
+    toks, lens = audio_to_token_ids(m, audio)
+    assert token_lists(toks, lens) == golden_json("decode_fwd.json")["results"]["b2_10s"]
+
+
+def test_int8_token_ids(va):
+    from velocity_asr import quantize as Q
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = Q.prepare_model_for_qat(m).to(DEV).eval()
+    audio = torch.from_numpy(S.make_audio(2, 48000, seed=21)).to(DEV)
+    mel = va.compute_mel_spectrogram(audio)
+    Q.calibrate_from_activations(m, mel)
+    assert np.array_equal(m.token_ids(mel).cpu().numpy(), m(mel).argmax(-1).cpu().numpy())

@@ -79,6 +79,14 @@ __global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict_
     }
 }
 
+__global__ void argmax_keys_kernel(unsigned long long* keys, int rows, int32_t* out, int reset) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    const unsigned long long k = keys[i];
+    out[i] = (int32_t)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
+    if (reset) keys[i] = 0ull;
+}
+
 }  // namespace
 }  // namespace vasr
 
@@ -102,4 +110,13 @@ VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int
     hipLaunchKernelGGL(collapse_kernel, dim3(B), dim3(64), 0, as_stream(stream), pred, L, blank, collapse, out_tokens,
                        out_len, out_start, out_end);
     return launch_status("vasr_ctc_collapse");
+}
+
+VASR_API int vasr_argmax_keys(uint64_t* keys, int rows, int32_t* out, int reset, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(keys && out && rows >= 0, "vasr_argmax_keys: bad arguments");
+    if (rows == 0) return VASR_OK;
+    hipLaunchKernelGGL(argmax_keys_kernel, dim3((rows + 255) / 256), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<unsigned long long*>(keys), rows, out, reset);
+    return launch_status("vasr_argmax_keys");
 }

@@ -123,6 +123,48 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
                 }
             }
         }
+    } else if constexpr (EPI == VASR_EPI_ARGMAX) {
+        // per row: this lane's best over its TN columns (ascending, strict > keeps the first),
+        // a 32-lane max of order-preserving (value, ~index) keys, one atomic per row and wave
+        unsigned long long* __restrict__ keys =
+            reinterpret_cast<unsigned long long*>(p.C) + (int64_t)t.bz * p.stride_c;
+        float bv[TN];
+        float4 qc[TN];
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+            const int col = n0 + wc * 32 * TN + tn * 32 + r;
+            const bool ok = !GUARD || col < p.N;
+            bv[tn] = (p.bias && ok) ? p.bias[col] : 0.0f;
+            if (p.qp) qc[tn] = ok ? p.qp[col] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                unsigned long long key = 0ull;
+#pragma unroll
+                for (int tn = 0; tn < TN; ++tn) {
+                    const int col = n0 + wc * 32 * TN + tn * 32 + r;
+                    if (GUARD && col >= p.N) continue;
+                    float v = acc[tm][tn][i];
+                    if (p.bias) v = v + bv[tn];
+                    if (p.qp) v = fake_quant(v, qc[tn]);
+                    const unsigned u = __float_as_uint(v);
+                    const unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+                    const unsigned long long k = ((unsigned long long)ord << 32) | (0xFFFFFFFFu - (unsigned)col);
+                    key = k > key ? k : key;
+                }
+#pragma unroll
+                for (int o = 1; o < 32; o <<= 1) {
+                    const unsigned lo = __shfl_xor((unsigned)key, o, 64);
+                    const unsigned hi = __shfl_xor((unsigned)(key >> 32), o, 64);
+                    const unsigned long long k = ((unsigned long long)hi << 32) | lo;
+                    key = k > key ? k : key;
+                }
+                if (r == 0 && (!GUARD || row < p.M) && key != 0ull) atomicMax(keys + row, key);
+            }
+        }
     } else {
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
@@ -212,7 +254,9 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
                    "%s: K, lda, stride_a must be multiples of 4 (K=%d lda=%lld)", fn, a->K, (long long)a->lda);
     VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->A) & 15) == 0, "%s: A must be 16-byte aligned", fn);
     const int epi = a->epilogue;
-    VASR_CHECK_ARG(epi >= VASR_EPI_NONE && epi <= VASR_EPI_PAIR_FUSION, "%s: unknown epilogue %d", fn, epi);
+    VASR_CHECK_ARG(epi >= VASR_EPI_NONE && epi <= VASR_EPI_ARGMAX, "%s: unknown epilogue %d", fn, epi);
+    if (epi == VASR_EPI_ARGMAX)
+        VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->C) & 7) == 0, "%s: argmax keys must be 8-byte aligned", fn);
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     if (pair)
         VASR_CHECK_ARG(a->N % 64 == 0 && a->n_out > 0 && a->n_out <= a->N / 2,

@@ -348,6 +348,7 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
         case VASR_EPI_PAIR_POWER:
             if constexpr (TN % 2 == 0) { VASR_L(VASR_EPI_PAIR_POWER); break; }
             set_error("vasr_linear_x3_f32: paired epilogue needs an even TN"); return VASR_EINVAL;
+        case VASR_EPI_ARGMAX: VASR_L(VASR_EPI_ARGMAX); break;
         case VASR_EPI_PAIR_FUSION:
             if constexpr (TN % 2 == 0) { VASR_L(VASR_EPI_PAIR_FUSION); break; }
             set_error("vasr_linear_x3_f32: paired epilogue needs an even TN"); return VASR_EINVAL;

@@ -67,13 +67,50 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nrows = min(TT, L - t0) + Kc - 1;
     const float* xb = x + (int64_t)b * L * C;
-    for (int rr = wave; rr < nrows; rr += 4) {
+    // Each wave normalises rows wave, wave + 4, ...: all of its row loads are issued before
+    // the first reduction, so the rows' load latencies and butterfly chains overlap.
+    constexpr int RPW = (TT + kMaxK - 1 + 3) / 4;
+    constexpr int CPL = kMaxC / 64;
+    float v[RPW][CPL];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const int rr = wave + 4 * i;
+        const int t = t0 - (Kc - 1) + rr;
+        const bool ok = rr < nrows && t >= 0;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int col = c * 64 + lane;
+            v[i][c] = (ok && col < C) ? xb[(int64_t)t * C + col] : 0.f;
+        }
+    }
+    float mean[RPW], rstd[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        float sum = 0.f;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) sum += v[i][c];
+        mean[i] = wave_sum(sum) / (float)C;
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        float q = 0.f;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const float d = (c * 64 + lane < C) ? v[i][c] - mean[i] : 0.f;
+            q += d * d;
+        }
+        rstd[i] = 1.0f / sqrtf(wave_sum(q) / (float)C + eps);
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+        const int rr = wave + 4 * i;
+        if (rr >= nrows) continue;
         const int t = t0 - (Kc - 1) + rr;
         float* dst = tile + rr * C;
-        if (t < 0) {
-            for (int c = lane; c < C; c += 64) dst[c] = 0.f;  // causal zero padding
-        } else {
-            ln_row_to(xb + (int64_t)t * C, ln_w, ln_b, dst, C, eps, lane);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int col = c * 64 + lane;
+            if (col < C) dst[col] = t < 0 ? 0.f : (v[i][c] - mean[i]) * rstd[i] * ln_w[col] + ln_b[col];
         }
     }
     __syncthreads();

@@ -20,7 +20,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libvasr_hip.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "vasr.h"))
 
-EPI_NONE, EPI_GELU, EPI_SOFTPLUS_FROM, EPI_RESIDUAL, EPI_GELU_PE, EPI_PAIR_POWER, EPI_PAIR_FUSION = range(7)
+(EPI_NONE, EPI_GELU, EPI_SOFTPLUS_FROM, EPI_RESIDUAL, EPI_GELU_PE, EPI_PAIR_POWER, EPI_PAIR_FUSION,
+ EPI_ARGMAX) = range(8)
 
 c_i32, c_i64, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -67,6 +68,7 @@ _SIGNATURES = {
     "vasr_fakequant_f32": ([c_p, c_i64, c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, ctypes.c_int, c_f32, c_f32,
                             c_p], ctypes.c_int),
     "vasr_minmax_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p], ctypes.c_int),
+    "vasr_argmax_keys": ([c_p, ctypes.c_int, c_p, ctypes.c_int, c_p], ctypes.c_int),
     "vasr_ctc_collapse": ([c_p] + [ctypes.c_int] * 4 + [c_p, c_p, c_p, c_p, c_p], ctypes.c_int),
 }
 

@@ -127,6 +127,15 @@ class CTCOutputHead(nn.Module):
         Q.record(self.proj[2], logits)
         return logits.view(B, L, w.shape[0])
 
+    def argmax(self, x: torch.Tensor) -> torch.Tensor:
+        """argmax over the vocabulary of forward(x), (B, L) int32, fused into the head GEMM: the
+        (B, L, V) logits are never written (SURVEY §8 f, rank 1)."""
+        B, L, D = x.shape
+        ln = self.proj[0]
+        w, b, qp = Q.linear_parts(self.proj[2])
+        h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
+        return ops.gemm_argmax(h.view(B * L, D), w, b, qparams=qp).view(B, L)
+
 
 class VELOCITYASR(nn.Module):
     """VELOCITY-ASR v2 (reference model.py:242-471)."""
@@ -183,6 +192,19 @@ class VELOCITYASR(nn.Module):
             return logits, {"temporal_binding": x, "local_features": local_features,
                             "fused_features": fused_features}
         return logits
+
+    def token_ids(self, mel_spectrogram: torch.Tensor) -> torch.Tensor:
+        """argmax(forward(mel), -1) as (B, L) int32 on the device, without materialising logits
+        (the CTC head's GEMM reduces each row in its epilogue).  Identical to the argmax of
+        forward()'s logits: same GEMM, same accumulation order."""
+        if mel_spectrogram.device.type != "cuda":
+            _lib.require_device()
+            raise RuntimeError("velocity_asr (MI355X build): token_ids needs HIP tensors")
+        with torch.no_grad():
+            x = self.temporal_binding(mel_spectrogram.to(torch.float32))
+            x = self.local_ssm(x)
+            x = self.global_context(x)
+            return self.ctc_head.argmax(x)
 
     def get_output_length(self, input_length: int) -> int:
         return (input_length + 1) // 2

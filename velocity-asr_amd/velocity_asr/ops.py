@@ -217,6 +217,34 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     return out
 
 
+def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+                qparams: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int32 argmax over the N outputs of a @ w.T + bias (after qparams) per row, fused into the
+    GEMM epilogue (VASR_EPI_ARGMAX): the (M, N) product is never written.  Ties -> first index."""
+    _cuda_f32("gemm_argmax.a", a)
+    _cuda_w("gemm_argmax.w", w)
+    bias = f32(bias)
+    M, K, lda = _rows("gemm_argmax.a", a)
+    N, Kw, ldw = _rows("gemm_argmax.w", w)
+    if Kw != K:
+        raise ValueError(f"gemm_argmax: a has K={K} but w has K={Kw}")
+    keys = torch.zeros(M, device=a.device, dtype=torch.int64)
+    out = torch.empty(M, device=a.device, dtype=torch.int32)
+    args = GemmArgs()
+    args.A, args.lda, args.stride_a = a.data_ptr(), lda, 0
+    args.W, args.ldw = w.data_ptr(), ldw
+    args.bias = ptr(bias)
+    args.C, args.ldc, args.stride_c = keys.data_ptr(), 1, 0
+    args.batch, args.M, args.N, args.K = 1, M, N, K
+    args.epilogue = L.EPI_ARGMAX
+    args.qparams = _qp(qparams, N)
+    ev = _t0("gemm")
+    _linear(args, w, stream_of(a))
+    _t1("gemm", ev, dict(M=M, N=N, K=K, batch=1))
+    check(L.lib().vasr_argmax_keys(keys.data_ptr(), M, out.data_ptr(), 0, stream_of(a)), "vasr_argmax_keys")
+    return out
+
+
 def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch: int, K: int, w: torch.Tensor,
                  bias: Optional[torch.Tensor], out: torch.Tensor, ldc: int, stride_c: int, *,
                  epilogue: int = L.EPI_NONE, aux: Optional[torch.Tensor] = None, ld_aux: int = 0,

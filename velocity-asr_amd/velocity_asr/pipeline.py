@@ -1,6 +1,7 @@
 """Batch transcription pipeline on the device: audio (B, S) -> tokens, no host round trip.
 
-    mel (reflect pad + DFT GEMM + log-mel)  ->  VELOCITYASR.forward  ->  argmax  ->  CTC collapse
+    mel (reflect pad + DFT GEMM + log-mel)  ->  VELOCITYASR.token_ids (forward with the CTC head's
+    row argmax fused into its GEMM)  ->  CTC collapse
 
 Everything stays in HBM; the only device->host traffic is the (B, L) int32 token block
 and lengths when the caller asks for Python lists.  ``GraphedTranscriber`` captures the
@@ -22,8 +23,7 @@ from .model import VELOCITYASR
 def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """(B, S) float32 HIP audio -> (tokens (B, L) int32, lengths (B,) int32), all on the device."""
     mel = mel_on_device(audio, SAMPLE_RATE, N_FFT, HOP_LENGTH, model.config.mel_bins)
-    logits = model(mel)
-    pred = ops.argmax(logits)
+    pred = model.token_ids(mel)  # CTC head GEMM with the row argmax fused: no logits in HBM
     toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False)
     return toks, lens
 

@@ -20,7 +20,7 @@ import torch
 
 from . import ops
 from .audio import HOP_LENGTH, SAMPLE_RATE, load_audio, mel_on_device
-from .decode import CTCDecoder, greedy_token_ids
+from .decode import CTCDecoder
 
 logger = logging.getLogger(__name__)
 
@@ -73,10 +73,11 @@ def _decode_batch(model, audio: torch.Tensor, decoder: CTCDecoder, timestamps: b
     """(b, S) device audio -> [(text, words or None)] through the device pipeline."""
     with torch.no_grad():
         mel = mel_on_device(audio, n_mels=model.config.mel_bins)
-        logits = model(mel)
         if beam_width > 1:
+            logits = model(mel)
             return [(t, None) for t in decoder.decode_beam_search(logits, beam_width=beam_width)]
-        toks, lens, st, en = greedy_token_ids(logits, decoder.blank_token, True, timestamps)
+        # greedy: the CTC head's GEMM reduces each frame to its argmax (no logits in HBM)
+        toks, lens, st, en = ops.ctc_collapse(model.token_ids(mel), decoder.blank_token, True, timestamps)
     toks, lens = toks.cpu().numpy(), lens.cpu().numpy()
     if timestamps:
         st, en = st.cpu().numpy(), en.cpu().numpy()
