@@ -118,7 +118,9 @@ def main():
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=3)
-    ap.add_argument("--streams", type=int, default=1, help="utterance groups replayed on concurrent HIP streams")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="utterance groups replayed as separate HIP graphs on concurrent streams (the scan of one "
+                         "group overlaps the GEMMs of the other; results are bitwise those of one graph)")
     ap.add_argument("--int8", action="store_true",
                     help="BASELINE configs[4]: INT8 fake-quant model (prepare_model_for_qat + activation calibration)")
     ap.add_argument("--bf16", action="store_true",
@@ -175,8 +177,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # token checksum over all ranks (tiny gather, outside the timed region)
+    # token checksum over all ranks (tiny gather, outside the timed region); the timed graph's
+    # own output must equal an eager pass over the same audio
     toks, lens = audio_to_token_ids(model, audio)
+    graph_match = True
+    if not args.eager:
+        from velocity_asr.pipeline import token_lists
+        gt, gl = tr.collect()
+        graph_match = token_lists(gt, gl) == token_lists(toks, lens)
     valid = torch.arange(toks.shape[1], device=dev)[None, :] < lens[:, None]
     csum = torch.tensor([float(lens.sum().item()), float(toks.long().masked_fill(~valid, 0).sum().item())],
                         device=dev, dtype=torch.float64)
@@ -243,6 +251,7 @@ def main():
                          ms_per_step=round(gm["total"] * 1e3, 3), tflops=round(gm["tflops"], 2)),
         },
         "token_checksum": [int(csum[0].item()), int(csum[1].item())],
+        "graph_tokens_match_eager": graph_match,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

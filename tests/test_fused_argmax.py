@@ -85,3 +85,21 @@ def test_int8_token_ids(va):
     mel = va.compute_mel_spectrogram(audio)
     Q.calibrate_from_activations(m, mel)
     assert np.array_equal(m.token_ids(mel).cpu().numpy(), m(mel).argmax(-1).cpu().numpy())
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_graphed_streams_match_eager(va, streams):
+    """The bench's timed path: utterance groups as HIP graphs on concurrent streams."""
+    from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids, token_lists
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    audio = torch.from_numpy(S.make_audio(4, 48000, seed=8)).to(DEV)
+    te, le = audio_to_token_ids(m, audio)
+    gt = GraphedTranscriber(m, 4, 48000, streams=streams)
+    gt.audio.copy_(audio)
+    gt.step()
+    gt.step()
+    torch.cuda.synchronize()
+    assert token_lists(*gt.collect()) == token_lists(te, le)

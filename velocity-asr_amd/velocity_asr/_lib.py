@@ -17,7 +17,8 @@ import torch
 
 ABI_VERSION = 3
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libvasr_hip.so")
+# VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
+LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "vasr.h"))
 
 (EPI_NONE, EPI_GELU, EPI_SOFTPLUS_FROM, EPI_RESIDUAL, EPI_GELU_PE, EPI_PAIR_POWER, EPI_PAIR_FUSION,
