@@ -223,6 +223,17 @@ int vasr_argmax_f32(const float* logits, int64_t ld, int rows, int V, int32_t* o
  * The fused CTC head (model.py:223-227 + decode.py:46) never writes the (rows, V) logits. */
 int vasr_argmax_keys(uint64_t* keys, int rows, int32_t* out, int reset, void* stream);
 
+/* CTC prefix beam search (decode.py:128-217, lm_scorer = None), one workgroup per utterance.
+ * logits: (B, L, V) with row stride ld_row and utterance stride ld_utt; W <= 32 beams.
+ * Outputs per utterance b, beam r < out_nbeams[b] (sorted as the reference returns them):
+ * out_tokens[(b*W + r)*L + 0 .. out_len[b*W + r]), out_score[b*W + r] (float64 sum of the
+ * float32 log-softmax values, as the reference's Python floats).  trie: caller workspace of
+ * B * vasr_ctc_beam_workspace_elems(L, W) int32. */
+int vasr_ctc_beam_search(const float* logits, int64_t ld_row, int64_t ld_utt, int B, int L, int V,
+                         int W, int blank, int32_t* trie, int32_t* out_tokens, int32_t* out_len,
+                         double* out_score, int32_t* out_nbeams, void* stream);
+int64_t vasr_ctc_beam_workspace_elems(int L, int W);
+
 /* Greedy CTC collapse per utterance (decode.py:51-69, :89-123): drop blank (and reset
  * prev), skip repeats of prev if collapse != 0.  out_tokens (B, L) holds each
  * utterance's kept tokens left-aligned, out_len (B) their counts.  If out_start /

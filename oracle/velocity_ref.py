@@ -509,3 +509,38 @@ def ctc_greedy_decode_with_timestamps(logits: np.ndarray, blank: int = 0):
             ts.append((start, len(row)))
         results.append((toks, ts))
     return results
+
+
+def log_softmax(x: np.ndarray) -> np.ndarray:
+    """F.log_softmax over the last dim in float32: (x - max) - log(sum(exp(x - max)))."""
+    x = np.asarray(x, f32)
+    m = x.max(axis=-1, keepdims=True)
+    d = (x - m).astype(f32)
+    return (d - np.log(np.exp(d).sum(axis=-1, keepdims=True, dtype=f32))).astype(f32)
+
+
+def ctc_beam_search(logits: np.ndarray, beam_width: int = 10, blank: int = 0):
+    """ctc_beam_search (decode.py:128-217), lm_scorer None: prefix beams keyed by the collapsed
+    prefix, strict-greater updates in insertion order, stable sort by score, float64 scores.
+    Returns per utterance a list of (tokens, score)."""
+    lp_all = log_softmax(logits)
+    out = []
+    for b in range(lp_all.shape[0]):
+        beams = {(): (0.0, None)}
+        for t in range(lp_all.shape[1]):
+            lp = lp_all[b, t]
+            new = {}
+            for prefix, (score, last) in beams.items():
+                s = score + float(lp[blank])
+                if prefix not in new or new[prefix][0] < s:
+                    new[prefix] = (s, blank)
+                for tok in range(lp.shape[0]):
+                    if tok == blank:
+                        continue
+                    s = score + float(lp[tok])
+                    key = prefix if last == tok else prefix + (tok,)
+                    if key not in new or new[key][0] < s:
+                        new[key] = (s, tok)
+            beams = dict(sorted(new.items(), key=lambda kv: kv[1][0], reverse=True)[:beam_width])
+        out.append([(list(p), sc) for p, (sc, _) in sorted(beams.items(), key=lambda kv: kv[1][0], reverse=True)])
+    return out

@@ -407,6 +407,28 @@ def gen_int8():
     save("int8_b2_3s.npz", **out)
 
 
+# --------------------------------------------------------------------------- beam search
+def gen_beam():
+    """ctc_beam_search (decode.py:128-217) on the decode.json logit cases and on soft random
+    logits (many competing prefixes), beam widths 1, 3, 5, 10."""
+    rng = np.random.default_rng(81)
+    dec = json.load(open(os.path.join(HERE, "decode.json")))
+    cases = {k: np.array(v["logits"], np.float32) for k, v in dec["cases"].items()}
+    cases["soft_v6"] = (rng.standard_normal((2, 30, 6)) * 1.5).astype(np.float32)
+    cases["soft_v40"] = (rng.standard_normal((2, 25, 40)) * 2.0).astype(np.float32)
+    cases["soft_l0"] = np.zeros((1, 0, 5), np.float32)
+    out = {"meta": json.loads(str(meta())), "cases": {}}
+    for name, lg in cases.items():
+        res = {}
+        for w in (1, 3, 5, 10):
+            r = ref_decode.ctc_beam_search(torch.from_numpy(lg), beam_width=w)
+            res[str(w)] = [[[list(map(int, d.tokens)), float(d.score)] for d in beams] for beams in r]
+        out["cases"][name] = {"logits": lg.tolist() if name.startswith("soft") else None, "beams": res}
+    with open(os.path.join(HERE, "beam.json"), "w") as f:
+        json.dump(out, f)
+    print("wrote beam.json")
+
+
 # --------------------------------------------------------------------------- bf16 (C3)
 def gen_bf16():
     """The reference run as a bf16 model: model.to(torch.bfloat16), fp32 audio -> mel, mel cast
@@ -428,7 +450,7 @@ def gen_bf16():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8", "bf16"]
+    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8", "bf16", "beam"]
     if "mel" in which:
         gen_mel()
     if "scan" in which:
@@ -445,3 +467,5 @@ if __name__ == "__main__":
         gen_int8()
     if "bf16" in which:
         gen_bf16()
+    if "beam" in which:
+        gen_beam()

@@ -68,14 +68,25 @@ def ctc_greedy_decode_with_timestamps(logits: torch.Tensor,
 
 def ctc_beam_search(logits: torch.Tensor, beam_width: int = 10, blank_token: int = BLANK_TOKEN,
                     lm_weight: float = 0.0, lm_scorer: Optional[Any] = None) -> List[List[DecodingResult]]:
-    """Prefix beam search with the reference's exact bookkeeping (decode.py:128-217).
+    """Prefix beam search (reference decode.py:128-217) on the HIP device.
 
-    log_softmax is computed on the device (one argmax-style row kernel pass is not needed:
-    torch's log_softmax on the HIP tensor); the beam bookkeeping is host logic over the
-    (L, V) score rows, vectorised per beam but keeping the reference's insertion order
-    and strict-greater update rule so ties resolve identically.
+    Without a language model the whole search runs in vasr_ctc_beam_search (one workgroup
+    per utterance, prefixes as trie nodes, the reference's insertion-order tie rules).  An
+    lm_scorer is a Python callable, so with one (or beam_width > 32) the search runs on the
+    host with the same bookkeeping over device-computed log-probabilities.
     """
     logits = _on_device(logits)
+    if (lm_scorer is None or lm_weight <= 0) and 1 <= beam_width <= 32:
+        toks, lens, scores, nb = ops.ctc_beam_search(logits.float(), beam_width, blank_token)
+        toks, lens, scores, nb = toks.cpu().numpy(), lens.cpu().numpy(), scores.cpu().numpy(), nb.cpu().numpy()
+        return [[DecodingResult(text="", tokens=toks[b, r, :lens[b, r]].tolist(), score=float(scores[b, r]))
+                 for r in range(int(nb[b]))] for b in range(toks.shape[0])]
+    return _ctc_beam_search_host(logits, beam_width, blank_token, lm_weight, lm_scorer)
+
+
+def _ctc_beam_search_host(logits: torch.Tensor, beam_width: int, blank_token: int, lm_weight: float,
+                          lm_scorer: Optional[Any]) -> List[List[DecodingResult]]:
+    """Host form of the same search (used with a Python lm_scorer)."""
     log_probs = torch.log_softmax(logits, dim=-1).cpu().numpy().astype(np.float64)
     B, L, V = log_probs.shape
     all_results = []

@@ -475,3 +475,24 @@ def minmax(x: torch.Tensor, per_channel: bool = False) -> Tuple[torch.Tensor, to
     check(lib.vasr_minmax_f32(hi.data_ptr(), rows, 1, rows, scratch.data_ptr(), hi1.data_ptr(), stream_of(x)),
           "vasr_minmax_f32")
     return lo1, hi1
+
+
+def ctc_beam_search(logits: torch.Tensor, beam_width: int, blank: int = 0):
+    """Device prefix beam search over (B, L, V) logits -> (tokens (B, W, L) int32, lengths (B, W),
+    scores (B, W) float64, beams per utterance (B,)), all on the device."""
+    _cuda_f32("ctc_beam_search.logits", logits)
+    if logits.dim() != 3:
+        raise ValueError("ctc_beam_search: logits must be (B, L, V)")
+    x = logits if logits.stride(-1) == 1 else logits.contiguous()
+    B, Lq, V = x.shape
+    W = int(beam_width)
+    dev = x.device
+    trie = torch.empty(max(B, 1) * int(L.lib().vasr_ctc_beam_workspace_elems(Lq, W)), device=dev, dtype=torch.int32)
+    toks = torch.zeros((B, W, max(Lq, 1)), device=dev, dtype=torch.int32)
+    lens = torch.zeros((B, W), device=dev, dtype=torch.int32)
+    scores = torch.zeros((B, W), device=dev, dtype=torch.float64)
+    nbeams = torch.zeros((B,), device=dev, dtype=torch.int32)
+    check(L.lib().vasr_ctc_beam_search(x.data_ptr(), x.stride(1), x.stride(0), B, Lq, V, W, int(blank), trie.data_ptr(),
+                                       toks.data_ptr(), lens.data_ptr(), scores.data_ptr(), nbeams.data_ptr(),
+                                       stream_of(x)), "vasr_ctc_beam_search")
+    return toks, lens, scores, nbeams
