@@ -173,6 +173,8 @@ int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t stride_p
                           const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
                           float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
                           int normalize, float* workspace, void* stream);
+/* workspace size of vasr_mel_log_norm_f32 in floats (log-mel rows + per-chunk fp64 partials) */
+int64_t vasr_mel_workspace_floats(int B, int F, int n_mels);
 
 /* Write (B, F, C) rows into a zero-padded frame layout: out[b][off + f][c] = x[b][f][c]
  * and zero for the other out_frames - F frames (batch stride out_frames * C).  Feeds mel

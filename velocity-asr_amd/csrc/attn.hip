@@ -30,54 +30,62 @@ constexpr int kMaxKeys = 64;
 constexpr int kMaxHd = 32;
 constexpr int kMaxA = 256;  // heads * head_dim (LDS: Kp * 2A floats <= 128 KiB)
 
-// grid (ceil(L*heads/256), B); one thread per (token, head).
+// grid (ceil(L*heads/256), B); one thread per (token, head).  HD = head_dim as a compile-time
+// constant (the model's 12, and 8 / 16), 0 = runtime head_dim <= kMaxHd with guarded loops.
+template <int HD>
 __global__ __launch_bounds__(256) void pooled_attention_kernel(const float* __restrict__ q, int64_t ld_q,
                                                                const float* __restrict__ kv, float* __restrict__ out,
-                                                               int L, int Kp, int heads, int hd) {
+                                                               int L, int Kp, int heads, int hd_rt) {
+    constexpr int JM = HD ? HD : kMaxHd;
+    const int hd = HD ? HD : hd_rt;
     extern __shared__ __attribute__((aligned(16))) float kvs[];  // Kp x 2A
     const int b = blockIdx.y;
     const int A = heads * hd;
     const float* kvb = kv + (int64_t)b * Kp * 2 * A;
-    for (int i = threadIdx.x; i < Kp * 2 * A; i += blockDim.x) kvs[i] = kvb[i];
-    __syncthreads();
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= L * heads) return;
-    const int t = idx / heads, hh = idx - t * heads;
+    const bool live = idx < L * heads;
+    const int t = live ? idx / heads : 0, hh = live ? idx - t * heads : 0;
+    // issue the query loads before the K/V staging so both latencies overlap
     const float* qr = q + ((int64_t)b * L + t) * ld_q + hh * hd;
-    float qv[kMaxHd];
+    float qv[JM];
 #pragma unroll
-    for (int j = 0; j < kMaxHd; ++j) qv[j] = j < hd ? qr[j] : 0.f;
+    for (int j = 0; j < JM; ++j) qv[j] = (live && j < hd) ? qr[j] : 0.f;
+    const int n4 = (Kp * 2 * A) / 4;  // K/V set is whole float4s (A % 4 == 0 is checked)
+    for (int i = threadIdx.x; i < n4; i += blockDim.x)
+        reinterpret_cast<float4*>(kvs)[i] = reinterpret_cast<const float4*>(kvb)[i];
+    __syncthreads();
+    if (!live) return;
     const float scale = sqrtf((float)hd);
     float mx = -INFINITY;
     for (int k = 0; k < Kp; ++k) {
         const float* kr = kvs + k * 2 * A + hh * hd;
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < kMaxHd; ++j)
+        for (int j = 0; j < JM; ++j)
             if (j < hd) s = __builtin_fmaf(qv[j], kr[j], s);
         mx = fmaxf(mx, s / scale);
     }
-    float acc[kMaxHd];
+    float acc[JM];
 #pragma unroll
-    for (int j = 0; j < kMaxHd; ++j) acc[j] = 0.f;
+    for (int j = 0; j < JM; ++j) acc[j] = 0.f;
     float sum = 0.f;
     for (int k = 0; k < Kp; ++k) {
         const float* kr = kvs + k * 2 * A + hh * hd;
         const float* vr = kvs + k * 2 * A + A + hh * hd;
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < kMaxHd; ++j)
+        for (int j = 0; j < JM; ++j)
             if (j < hd) s = __builtin_fmaf(qv[j], kr[j], s);
         const float p = expf(s / scale - mx);
         sum += p;
 #pragma unroll
-        for (int j = 0; j < kMaxHd; ++j)
+        for (int j = 0; j < JM; ++j)
             if (j < hd) acc[j] = __builtin_fmaf(p, vr[j], acc[j]);
     }
     const float inv = 1.0f / sum;
     float* orow = out + ((int64_t)b * L + t) * A + hh * hd;
 #pragma unroll
-    for (int j = 0; j < kMaxHd; ++j)
+    for (int j = 0; j < JM; ++j)
         if (j < hd) orow[j] = acc[j] * inv;
 }
 
@@ -107,7 +115,15 @@ VASR_API int vasr_pooled_attention_f32(const float* q, int64_t ld_q, const float
     const int work = L * heads;
     const size_t lds = (size_t)Kp * 2 * heads * head_dim * sizeof(float);
     VASR_CHECK_ARG(lds <= 65536, "vasr_pooled_attention_f32: K/V set exceeds 64 KiB of LDS");
-    hipLaunchKernelGGL(pooled_attention_kernel, dim3((work + 255) / 256, B), dim3(256), lds, as_stream(stream), q, ld_q,
-                       kv, out, L, Kp, heads, head_dim);
+    VASR_CHECK_ARG((heads * head_dim) % 4 == 0 && (reinterpret_cast<uintptr_t>(kv) & 15) == 0,
+                   "vasr_pooled_attention_f32: heads*head_dim must be a multiple of 4 and kv 16-byte aligned");
+    const dim3 grid((work + 255) / 256, B);
+    hipStream_t s = as_stream(stream);
+    switch (head_dim) {
+        case 8: hipLaunchKernelGGL(pooled_attention_kernel<8>, grid, dim3(256), lds, s, q, ld_q, kv, out, L, Kp, heads, 8); break;
+        case 12: hipLaunchKernelGGL(pooled_attention_kernel<12>, grid, dim3(256), lds, s, q, ld_q, kv, out, L, Kp, heads, 12); break;
+        case 16: hipLaunchKernelGGL(pooled_attention_kernel<16>, grid, dim3(256), lds, s, q, ld_q, kv, out, L, Kp, heads, 16); break;
+        default: hipLaunchKernelGGL(pooled_attention_kernel<0>, grid, dim3(256), lds, s, q, ld_q, kv, out, L, Kp, heads, head_dim);
+    }
     return launch_status("vasr_pooled_attention_f32");
 }

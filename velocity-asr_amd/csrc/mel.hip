@@ -144,6 +144,8 @@ VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t
     return launch_status("vasr_mel_log_norm_f32/norm");
 }
 
+VASR_API int64_t vasr_mel_workspace_floats(int B, int F, int n_mels) { return (int64_t)B * F * n_mels; }
+
 VASR_API int vasr_pad_frames_f32(const float* x, float* out, int out_frames, int off, int B, int F, int C,
                                  void* stream) {
     using namespace vasr;

@@ -356,7 +356,7 @@ def mel_log_norm(power: torch.Tensor, ld_power: int, stride_power: int, fb_csr, 
                  normalize: bool) -> torch.Tensor:
     rowptr, col, val = fb_csr
     out = torch.empty((B, F, n_mels), device=power.device, dtype=torch.float32)
-    ws = torch.empty((B, F, n_mels), device=power.device, dtype=torch.float32)
+    ws = torch.empty(int(L.lib().vasr_mel_workspace_floats(B, F, n_mels)), device=power.device, dtype=torch.float32)
     check(L.lib().vasr_mel_log_norm_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(), col.data_ptr(),
                                         val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F, n_mels, int(normalize),
                                         ws.data_ptr(), stream_of(power)), "vasr_mel_log_norm_f32")
