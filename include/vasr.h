@@ -59,9 +59,9 @@ enum vasr_epilogue {
     VASR_EPI_GELU_PE = 4,       /* C = gelu_erf(acc + bias) + aux[row][col] (pos. enc.) */
     VASR_EPI_PAIR_POWER = 5,    /* W rows paired in 32s (re|im): C[row][k] = re^2+im^2 */
     VASR_EPI_PAIR_FUSION = 6,   /* W rows paired (gate|global): gated fusion, see doc  */
-    VASR_EPI_ARGMAX = 7         /* row argmax of acc + bias (after qparams), no C write:
-                                   C is a uint64 key per row (batch stride stride_c), zeroed
-                                   by the caller and max-combined atomically; decode with
+    VASR_EPI_ARGMAX = 7         /* row argmax of acc + bias (after qparams), no logits write:
+                                   C is (rows, ldc) uint64 partial keys, one per 32 columns
+                                   (ldc >= ceil(N/32)), every slot written; decode with
                                    vasr_argmax_keys (ties -> first index, decode.py:46) */
 };
 
@@ -220,10 +220,11 @@ int vasr_minmax_f32(const float* x, int64_t ldx, int rows, int cols, float* out_
  */
 int vasr_argmax_f32(const float* logits, int64_t ld, int rows, int V, int32_t* out, void* stream);
 
-/* Row keys of a VASR_EPI_ARGMAX GEMM -> int32 argmax indices (rows entries); the keys are
- * zeroed again when reset != 0 (ready for the next fused GEMM, e.g. in a replayed graph).
- * The fused CTC head (model.py:223-227 + decode.py:46) never writes the (rows, V) logits. */
-int vasr_argmax_keys(uint64_t* keys, int rows, int32_t* out, int reset, void* stream);
+/* Partial keys of a VASR_EPI_ARGMAX GEMM ((rows, ld), `slots` = ceil(N/32) used) -> int32
+ * argmax indices.  Keys are order-preserving (float bits, ~column) pairs, so the largest is
+ * the largest logit with the smallest index.  The fused CTC head (model.py:223-227 +
+ * decode.py:46) never writes the (rows, V) logits. */
+int vasr_argmax_keys(const uint64_t* keys, int64_t ld, int slots, int rows, int32_t* out, void* stream);
 
 /* CTC prefix beam search (decode.py:128-217, lm_scorer = None), one workgroup per utterance.
  * logits: (B, L, V) with row stride ld_row and utterance stride ld_utt; W <= 32 beams.

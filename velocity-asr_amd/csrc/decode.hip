@@ -79,12 +79,25 @@ __global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict_
     }
 }
 
-__global__ void argmax_keys_kernel(unsigned long long* keys, int rows, int32_t* out, int reset) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= rows) return;
-    const unsigned long long k = keys[i];
-    out[i] = (int32_t)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
-    if (reset) keys[i] = 0ull;
+// One wave per two rows: lane l reads slot l % 32 of row 2w + l / 32 (coalesced), then a
+// 32-lane max by shuffles.
+__global__ __launch_bounds__(256) void argmax_keys_kernel(const unsigned long long* __restrict__ keys, int64_t ld,
+                                                          int slots, int rows, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+    const int sl = lane & 31;
+    unsigned long long k = 0ull;
+    if (row < rows)
+        for (int s = sl; s < slots; s += 32) {
+            const unsigned long long v = keys[(int64_t)row * ld + s];
+            k = v > k ? v : k;
+        }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(k, o, 64);
+        k = v > k ? v : k;
+    }
+    if (row < rows && sl == 0) out[row] = (int32_t)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
 }
 
 }  // namespace
@@ -112,11 +125,11 @@ VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int
     return launch_status("vasr_ctc_collapse");
 }
 
-VASR_API int vasr_argmax_keys(uint64_t* keys, int rows, int32_t* out, int reset, void* stream) {
+VASR_API int vasr_argmax_keys(const uint64_t* keys, int64_t ld, int slots, int rows, int32_t* out, void* stream) {
     using namespace vasr;
-    VASR_CHECK_ARG(keys && out && rows >= 0, "vasr_argmax_keys: bad arguments");
+    VASR_CHECK_ARG(keys && out && rows >= 0 && slots >= 1 && ld >= slots, "vasr_argmax_keys: bad arguments");
     if (rows == 0) return VASR_OK;
-    hipLaunchKernelGGL(argmax_keys_kernel, dim3((rows + 255) / 256), dim3(256), 0, as_stream(stream),
-                       reinterpret_cast<unsigned long long*>(keys), rows, out, reset);
+    hipLaunchKernelGGL(argmax_keys_kernel, dim3((rows + 7) / 8), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const unsigned long long*>(keys), ld, slots, rows, out);
     return launch_status("vasr_argmax_keys");
 }

@@ -60,6 +60,32 @@ __device__ __forceinline__ Tile decode_tile(const GemmParams& p) {
     return t;
 }
 
+// Max of a 64-bit key over the 32 lanes r = 0..31 of each wave half, all in DPP (no LDS
+// round trips): xor 1, xor 2 (quad_perm), the half-row and row mirrors complete each 16-lane
+// row; row_bcast15 then hands row 0's (2's) result to row 1 (3), whose lanes (r = 16..31)
+// all end with the max of the 32.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)v, (int)(unsigned)v, CTRL, ROWMASK, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(v >> 32), (int)(unsigned)(v >> 32), CTRL, ROWMASK, 0xF,
+                                               false);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+__device__ __forceinline__ unsigned long long max_u64_over_32_lanes(unsigned long long k) {
+    unsigned long long o;
+    o = dpp_u64<0xB1, 0xF>(k);  // quad_perm [1,0,3,2]
+    k = o > k ? o : k;
+    o = dpp_u64<0x4E, 0xF>(k);  // quad_perm [2,3,0,1]
+    k = o > k ? o : k;
+    o = dpp_u64<0x141, 0xF>(k);  // row_half_mirror
+    k = o > k ? o : k;
+    o = dpp_u64<0x140, 0xF>(k);  // row_mirror
+    k = o > k ? o : k;
+    o = dpp_u64<0x142, 0xA>(k);  // row_bcast15 into rows 1 and 3 (rows 0, 2 keep their own value)
+    return o > k ? o : k;
+}
+
 // Accumulator element i of MFMA tile (tm, tn) of wave (wr, wc), lane (r, h) is
 // C[m0 + wr*32*TM + tm*32 + (i&3) + 8*(i>>2) + 4*h][n0 + wc*32*TN + tn*32 + r].
 //
@@ -71,7 +97,7 @@ __device__ __forceinline__ Tile decode_tile(const GemmParams& p) {
 // GUARD = false for tiles wholly inside M x N: no per-element bounds branches.
 template <int TM, int TN, int EPI, bool GUARD>
 __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t, floatx16 (&acc)[TM][TN], int wr,
-                                              int wc, int r, int h) {
+                                              int wc, int r, int h, unsigned long long* scr) {
     float* __restrict__ Cb = p.C + (int64_t)t.bz * p.stride_c;
     const float* __restrict__ auxb = p.aux ? p.aux + (int64_t)t.bz * p.stride_aux : nullptr;
     const int m0 = t.m0, n0 = t.n0;
@@ -125,9 +151,12 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
         }
     } else if constexpr (EPI == VASR_EPI_ARGMAX) {
         // per row: this lane's best over its TN columns (ascending, strict > keeps the first),
-        // a 32-lane max of order-preserving (value, ~index) keys, one atomic per row and wave
+        // then the 32-lane max of order-preserving (value, ~index) keys; the wave's TN x 32
+        // columns form slots s0 .. s0+TN-1 of 32 columns: slot s0 gets the key, the others 0,
+        // so every slot of the row is written (plain stores, no atomics, no zero-init)
         unsigned long long* __restrict__ keys =
             reinterpret_cast<unsigned long long*>(p.C) + (int64_t)t.bz * p.stride_c;
+        const int s0 = (n0 + wc * 32 * TN) / 32;
         float bv[TN];
         float4 qc[TN];
 #pragma unroll
@@ -139,9 +168,9 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
         }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
+            unsigned long long kl[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
                 unsigned long long key = 0ull;
 #pragma unroll
                 for (int tn = 0; tn < TN; ++tn) {
@@ -155,14 +184,41 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
                     const unsigned long long k = ((unsigned long long)ord << 32) | (0xFFFFFFFFu - (unsigned)col);
                     key = k > key ? k : key;
                 }
+                kl[i] = key;
+            }
+            if (scr) {
+                // transpose through LDS: lane (r, h) writes its 16 row keys to column r of the
+                // wave's 32 rows (rows padded to 33 entries: conflict-free column reads), then
+                // lane (r, h) reduces half h of row r and the halves meet across h
 #pragma unroll
-                for (int o = 1; o < 32; o <<= 1) {
-                    const unsigned lo = __shfl_xor((unsigned)key, o, 64);
-                    const unsigned hi = __shfl_xor((unsigned)(key >> 32), o, 64);
-                    const unsigned long long k = ((unsigned long long)hi << 32) | lo;
+                for (int i = 0; i < 16; ++i) scr[((i & 3) + 8 * (i >> 2) + 4 * h) * 33 + r] = kl[i];
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+                __builtin_amdgcn_wave_barrier();
+                unsigned long long key = 0ull;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const unsigned long long k = scr[r * 33 + 16 * h + j];
                     key = k > key ? k : key;
                 }
-                if (r == 0 && (!GUARD || row < p.M) && key != 0ull) atomicMax(keys + row, key);
+                const unsigned long long o = __shfl_xor(key, 32, 64);
+                key = o > key ? o : key;
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();  // all reads done before the next tm overwrites scr
+                const int row = m0 + wr * 32 * TM + tm * 32 + r;
+                if (!GUARD || row < p.M) {
+#pragma unroll
+                    for (int sl = h; sl < TN; sl += 2)  // h = 0 writes the key slot, h = 1 the zero slots
+                        if (!GUARD || (s0 + sl) * 32 < p.N) keys[(int64_t)row * p.ldc + s0 + sl] = sl == 0 ? key : 0ull;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int row = m0 + wr * 32 * TM + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const unsigned long long key = max_u64_over_32_lanes(kl[i]);  // lanes r = 16..31 hold it
+                    const int slot = r - (32 - TN);  // lanes r = 32-TN .. 31 write slots s0 .. s0+TN-1
+                    if (slot >= 0 && (!GUARD || row < p.M) && (!GUARD || (s0 + slot) * 32 < p.N))
+                        keys[(int64_t)row * p.ldc + s0 + slot] = slot == 0 ? key : 0ull;
+                }
             }
         }
     } else {
@@ -203,14 +259,16 @@ __device__ __forceinline__ void epilogue_body(const GemmParams& p, const Tile& t
     }
 }
 
+// scr: optional per-wave LDS scratch of 32 x 33 uint64 for the ARGMAX row reduction (the
+// staging LDS is free once the main loop is done); null selects the DPP reduction.
 template <int BM, int BN, int TM, int TN, int EPI>
 __device__ __forceinline__ void epilogue(const GemmParams& p, const Tile& t, floatx16 (&acc)[TM][TN], int wr,
-                                         int wc, int r, int h) {
+                                         int wc, int r, int h, unsigned long long* scr = nullptr) {
     const int ncols = (EPI == VASR_EPI_PAIR_POWER || EPI == VASR_EPI_PAIR_FUSION) ? 2 * p.n_out : p.N;
     if (t.m0 + BM <= p.M && t.n0 + BN <= ncols)
-        epilogue_body<TM, TN, EPI, false>(p, t, acc, wr, wc, r, h);
+        epilogue_body<TM, TN, EPI, false>(p, t, acc, wr, wc, r, h, scr);
     else
-        epilogue_body<TM, TN, EPI, true>(p, t, acc, wr, wc, r, h);
+        epilogue_body<TM, TN, EPI, true>(p, t, acc, wr, wc, r, h, scr);
 }
 
 
@@ -256,7 +314,8 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
     const int epi = a->epilogue;
     VASR_CHECK_ARG(epi >= VASR_EPI_NONE && epi <= VASR_EPI_ARGMAX, "%s: unknown epilogue %d", fn, epi);
     if (epi == VASR_EPI_ARGMAX)
-        VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->C) & 7) == 0, "%s: argmax keys must be 8-byte aligned", fn);
+        VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(a->C) & 7) == 0 && a->ldc >= (a->N + 31) / 32,
+                       "%s: argmax keys must be 8-byte aligned with ldc >= ceil(N / 32) slots", fn);
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     if (pair)
         VASR_CHECK_ARG(a->N % 64 == 0 && a->n_out > 0 && a->n_out <= a->N / 2,

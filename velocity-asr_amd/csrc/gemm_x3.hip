@@ -328,7 +328,11 @@ __global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm
                 for (int i = 0; i < 16; ++i) sum += acc[tm][tn][i];
         if (sum != 1.2345f) return;
     }
-    epilogue<BM, BN, TM, TN, EPI>(p, t, acc, wr, wc, r, h);
+    // ARGMAX: each wave gets 32 x 33 uint64 of the (now idle) staging LDS, two waves per slot
+    unsigned long long* scr = nullptr;
+    if constexpr (EPI == VASR_EPI_ARGMAX && STAGE >= 2 * 32 * 33 * 8)  // else: the DPP reduction
+        scr = reinterpret_cast<unsigned long long*>(wave < 2 ? s0 : s1) + (wave & 1) * 32 * 33;
+    epilogue<BM, BN, TM, TN, EPI>(p, t, acc, wr, wc, r, h, scr);
 }
 
 template <int WM, int WN, int TM, int TN, int RING, int P>

@@ -70,7 +70,7 @@ _SIGNATURES = {
     "vasr_fakequant_f32": ([c_p, c_i64, c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, ctypes.c_int, c_f32, c_f32,
                             c_p], ctypes.c_int),
     "vasr_minmax_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p], ctypes.c_int),
-    "vasr_argmax_keys": ([c_p, ctypes.c_int, c_p, ctypes.c_int, c_p], ctypes.c_int),
+    "vasr_argmax_keys": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
     "vasr_ctc_beam_search": ([c_p, c_i64, c_i64] + [ctypes.c_int] * 5 + [c_p] * 5 + [c_p], ctypes.c_int),
     "vasr_ctc_beam_workspace_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_ctc_collapse": ([c_p] + [ctypes.c_int] * 4 + [c_p, c_p, c_p, c_p, c_p], ctypes.c_int),

@@ -228,20 +228,21 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     N, Kw, ldw = _rows("gemm_argmax.w", w)
     if Kw != K:
         raise ValueError(f"gemm_argmax: a has K={K} but w has K={Kw}")
-    keys = torch.zeros(M, device=a.device, dtype=torch.int64)
+    slots = (N + 31) // 32
+    keys = torch.empty((M, slots), device=a.device, dtype=torch.int64)  # every slot is written
     out = torch.empty(M, device=a.device, dtype=torch.int32)
     args = GemmArgs()
     args.A, args.lda, args.stride_a = a.data_ptr(), lda, 0
     args.W, args.ldw = w.data_ptr(), ldw
     args.bias = ptr(bias)
-    args.C, args.ldc, args.stride_c = keys.data_ptr(), 1, 0
+    args.C, args.ldc, args.stride_c = keys.data_ptr(), slots, 0
     args.batch, args.M, args.N, args.K = 1, M, N, K
     args.epilogue = L.EPI_ARGMAX
     args.qparams = _qp(qparams, N)
     ev = _t0("gemm")
     _linear(args, w, stream_of(a))
     _t1("gemm", ev, dict(M=M, N=N, K=K, batch=1))
-    check(L.lib().vasr_argmax_keys(keys.data_ptr(), M, out.data_ptr(), 0, stream_of(a)), "vasr_argmax_keys")
+    check(L.lib().vasr_argmax_keys(keys.data_ptr(), slots, slots, M, out.data_ptr(), stream_of(a)), "vasr_argmax_keys")
     return out
 
 

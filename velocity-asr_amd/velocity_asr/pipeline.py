@@ -11,6 +11,7 @@ the ~150 host launches per step from the critical path.
 
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -20,10 +21,17 @@ from .audio import HOP_LENGTH, N_FFT, N_MELS, SAMPLE_RATE, mel_on_device
 from .model import VELOCITYASR
 
 
+# VASR_FUSED_ARGMAX=0 selects logits + a separate argmax pass (diagnostic comparison)
+FUSED_ARGMAX = os.environ.get("VASR_FUSED_ARGMAX", "1") != "0"
+
+
 def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """(B, S) float32 HIP audio -> (tokens (B, L) int32, lengths (B,) int32), all on the device."""
     mel = mel_on_device(audio, SAMPLE_RATE, N_FFT, HOP_LENGTH, model.config.mel_bins)
-    pred = model.token_ids(mel)  # CTC head GEMM with the row argmax fused: no logits in HBM
+    if FUSED_ARGMAX:
+        pred = model.token_ids(mel)  # CTC head GEMM with the row argmax fused: no logits in HBM
+    else:
+        pred = ops.argmax(model(mel))
     toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False)
     return toks, lens
 
