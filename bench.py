@@ -51,13 +51,24 @@ def build_model(device):
     return m.to(device).eval()
 
 
-def kernel_roofline(model, audio, steps):
-    """Per-launch times of the scan and GEMM families over `steps` eager steps (HIP events)."""
+def kernel_roofline(model, audio, steps, streams=1):
+    """Per-launch times of the scan and GEMM families over `steps` eager steps (HIP events on
+    each launch's own stream), run as the timed graphs run: `streams` utterance groups issued
+    on concurrent streams, so the launches have the graph's shapes and the same overlap (and
+    a rocprofv3 trace of this command sees one population per kernel)."""
     from velocity_asr import ops
     from velocity_asr.pipeline import audio_to_token_ids
+    g = audio.shape[0] // streams
+    sts = [torch.cuda.Stream(audio.device) for _ in range(streams)]
+    main = torch.cuda.current_stream(audio.device)
     with ops.kernel_timer("ssm_scan", "gemm") as kt:
         for _ in range(steps):
-            audio_to_token_ids(model, audio)
+            for i, st in enumerate(sts):
+                st.wait_stream(main)
+                with torch.cuda.stream(st):
+                    audio_to_token_ids(model, audio[i * g:(i + 1) * g])
+            for st in sts:
+                main.wait_stream(st)
     rec = kt.summary()
     out = {}
     # selective scan of the 8 local blocks (N=64): bytes = B*L*(4*Di + 2*N)*4 per launch
@@ -68,7 +79,7 @@ def kernel_roofline(model, audio, steps):
         elems = i["B"] * i["L"] * i["Di"] * i["N"]
         t = float(np.mean([d for d, _ in scans]))
         out["scan"] = dict(t=t, bytes=bytes_per, elems=elems, launches=len(scans), per_step=len(scans) / steps,
-                           total=sum(d for d, _ in scans) / steps)
+                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"])
     g = rec["gemm"]
     flops = [2.0 * i["M"] * i["N"] * i["K"] * i["batch"] for _, i in g]
     groups = {}
@@ -191,7 +202,7 @@ def main():
     if world > 1:
         dist.all_reduce(csum)
 
-    rf = kernel_roofline(model, audio, args.roofline_steps)
+    rf = kernel_roofline(model, audio, args.roofline_steps, 1 if args.eager else args.streams)
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -219,7 +230,10 @@ def main():
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            roof["traffic"] = json.load(open(pmc)).get(key)
+            t = json.load(open(pmc)).get(key)
+            if isinstance(t, dict) and sc:  # by launch grid: B x Di/16 blocks of 256 threads
+                t = t.get(str(sc["B"] * (sc["Di"] // 16) * 256))
+            roof["traffic"] = t
         except Exception:
             pass
     line = {

@@ -55,26 +55,27 @@ def main(tag):
     rows = list(csv.DictReader(open(stats)))
     fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = pmc(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
-    per_kernel = {}
+    per_kernel = {}  # (kernel, grid) -> (read bytes, write bytes, launches)
     for key in set(fetch) | set(write):
         f = fetch.get(key, [0.0])
         w = write.get(key, [0.0])
-        per_kernel[key] = (2 * 1024 * sum(f) / len(f), 1024 * sum(w) / len(w))
+        per_kernel[key] = (2 * 1024 * sum(f) / len(f), 1024 * sum(w) / len(w), max(len(f), len(w)))
     lines = [f"# rocprofv3 summary, run {tag}", "",
              "| kernel | calls | avg us | share % | HBM read MB/launch | HBM write MB/launch |",
              "|---|---|---|---|---|---|"]
     traffic = {}
     for r in rows:
         n = short(r["Name"])
-        cands = [v for (k, g), v in per_kernel.items() if k == n]
-        rd = max((c[0] for c in cands), default=None)
-        wr = max((c[1] for c in cands), default=None)
+        # the launch population (grid size) with the most launches: the timed graphs' shape
+        cands = sorted(((v[2], g, v) for (k, g), v in per_kernel.items() if k == n), reverse=True)
+        rd = cands[0][2][0] if cands else None
+        wr = cands[0][2][1] if cands else None
         lines.append(f"| `{n[:70]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['Percentage']):.2f} | {'' if rd is None else f'{rd / 1e6:.1f}'} | "
                      f"{'' if wr is None else f'{wr / 1e6:.1f}'} |")
         fam = family(r["Name"])
         if fam in ("ssm_scan",) and rd is not None:
-            traffic[fam] = int(rd + wr)
+            traffic[fam] = {str(g): int(v[0] + v[1]) for _, g, v in cands}  # grid size -> bytes
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
