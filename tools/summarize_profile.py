@@ -79,7 +79,7 @@ def main(tag):
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
-        json.dump(dict(run=tag, unit="bytes per launch (FETCH_SIZE*2 + WRITE_SIZE)", **traffic), f, indent=1)
+        json.dump(dict(run=tag, unit="bytes per launch (FETCH_SIZE*2 + WRITE_SIZE), by launch grid size (threads)", **traffic), f, indent=1)
     print("\n".join(lines[:14]))
 
 
