@@ -96,6 +96,141 @@ __global__ __launch_bounds__(256) void mel_norm_kernel(const float* __restrict__
     }
 }
 
+// Chunked form of mel_log + mel_norm (used when the filterbank fits the LDS tables): blocks of
+// kFC frames per utterance, so the grid is B * ceil(F / kFC) blocks (1008 at B = 16, F = 1001):
+//  A (mel_chunk_log_kernel): stage the chunk's power rows (coalesced) and the CSR in LDS, write
+//    the log-mel rows to the workspace and per-(chunk, bin) fp64 sums of x and x^2;
+//  B (mel_chunk_norm_kernel): per bin, the chunk partials summed in chunk order (deterministic):
+//    mean = S / F, unbiased var = (Q - S mean) / (F - 1) in fp64 (exact mean for constant rows,
+//    so silent audio still gives 0), then the chunk's normalised rows.
+constexpr int kFC = 16;
+constexpr int kMaxLdp = 256;
+constexpr int kMaxNnz = 1024;
+constexpr int kMaxMels = 85;  // 3 bins-wide phases of a 256-thread block
+
+__global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restrict__ P, int64_t ldp, int64_t stridep,
+                                                            const int32_t* __restrict__ rowptr,
+                                                            const int32_t* __restrict__ col,
+                                                            const float* __restrict__ val, float* __restrict__ tmp,
+                                                            double* __restrict__ part, int F, int n_mels) {
+    __shared__ float rows[kFC * kMaxLdp];
+    __shared__ float vals[kFC * kMaxMels];
+    __shared__ int rp_s[kMaxMels + 1];
+    __shared__ int col_s[kMaxNnz];
+    __shared__ float val_s[kMaxNnz];
+    const int b = blockIdx.y, c = blockIdx.x, nch = gridDim.x;
+    const int f0 = c * kFC;
+    const int nf = min(kFC, F - f0);
+    const int nnz = rowptr[n_mels];
+    const bool csr_lds = nnz <= kMaxNnz;  // else read the CSR from global memory
+    for (int i = threadIdx.x; i <= n_mels; i += blockDim.x) rp_s[i] = rowptr[i];
+    if (csr_lds)
+        for (int i = threadIdx.x; i < nnz; i += blockDim.x) {
+            col_s[i] = col[i];
+            val_s[i] = val[i];
+        }
+    const float* Pb = P + (int64_t)b * stridep + (int64_t)f0 * ldp;
+    const int nrow = nf * (int)ldp;
+    for (int i0 = threadIdx.x; i0 < nrow; i0 += 8 * 256) {  // 8 independent loads in flight per thread
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (i0 + u * 256 < nrow) ? Pb[i0 + u * 256] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * 256 < nrow) rows[i0 + u * 256] = v[u];
+    }
+    __syncthreads();
+    float* tb = tmp + ((int64_t)b * F + f0) * n_mels;
+    for (int i = threadIdx.x; i < nf * n_mels; i += blockDim.x) {
+        const int fl = i / n_mels, m = i - fl * n_mels;
+        const float* prow = rows + fl * ldp;
+        float acc = 0.f;
+        if (csr_lds)
+            for (int e = rp_s[m]; e < rp_s[m + 1]; ++e) acc = __builtin_fmaf(val_s[e], prow[col_s[e]], acc);
+        else
+            for (int e = rp_s[m]; e < rp_s[m + 1]; ++e) acc = __builtin_fmaf(val[e], prow[col[e]], acc);
+        const float v = logf(acc + 1e-10f);
+        vals[i] = v;
+        tb[i] = v;
+    }
+    __syncthreads();
+    for (int m = threadIdx.x; m < n_mels; m += blockDim.x) {
+        double S = 0.0, Q = 0.0;
+        for (int fl = 0; fl < nf; ++fl) {
+            const double v = (double)vals[fl * n_mels + m];
+            S += v;
+            Q += v * v;
+        }
+        double* pp = part + (((int64_t)b * nch + c) * n_mels + m) * 2;
+        pp[0] = S;
+        pp[1] = Q;
+    }
+}
+
+// Per (b, bin): the chunk partials summed in a fixed order (3 interleaved phases, then the
+// phases in order) -> {mean, std + 1e-10} as floats.
+__global__ __launch_bounds__(256) void mel_chunk_stats_kernel(const double* __restrict__ part, float* __restrict__ stats,
+                                                              int nch, int F, int n_mels, int normalize) {
+    __shared__ double red[2][3][kMaxMels];
+    const int b = blockIdx.x;
+    const int m = threadIdx.x % n_mels, ph = threadIdx.x / n_mels;  // 3 phases of n_mels threads (n_mels <= 85)
+    const int nph = min(3, (int)blockDim.x / n_mels);
+    if (ph < nph) {
+        // four independent accumulator pairs (loads in flight together), combined in a fixed order
+        double S[4] = {0.0, 0.0, 0.0, 0.0}, Q[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = ph; k0 < nch; k0 += 4 * nph) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u * nph;
+                if (k < nch) {
+                    const double* pp = part + (((int64_t)b * nch + k) * n_mels + m) * 2;
+                    S[u] += pp[0];
+                    Q[u] += pp[1];
+                }
+            }
+        }
+        red[0][ph][m] = (S[0] + S[1]) + (S[2] + S[3]);
+        red[1][ph][m] = (Q[0] + Q[1]) + (Q[2] + Q[3]);
+    }
+    __syncthreads();
+    if (threadIdx.x < n_mels) {
+        double S = 0.0, Q = 0.0;
+        for (int q = 0; q < nph; ++q) {
+            S += red[0][q][m];
+            Q += red[1][q][m];
+        }
+        float mean = 0.f, denom = 1.f;
+        if (normalize) {
+            const double mu = S / (double)F;
+            // unbiased (torch.std default); F == 1 gives nan like the reference
+            const double var = fmax(Q - S * mu, 0.0) / (double)(F - 1);
+            mean = (float)mu;
+            denom = (float)sqrt(var) + 1e-10f;
+        }
+        stats[((int64_t)b * n_mels + m) * 2] = mean;
+        stats[((int64_t)b * n_mels + m) * 2 + 1] = denom;
+    }
+}
+
+__global__ __launch_bounds__(256) void mel_chunk_norm_kernel(const float* __restrict__ tmp,
+                                                             const float* __restrict__ stats, float* __restrict__ out,
+                                                             int64_t out_stride, int frame_off, int F, int n_mels,
+                                                             int normalize) {
+    __shared__ float st_s[2 * kMaxMels];
+    const int b = blockIdx.y, c = blockIdx.x;
+    const int f0 = c * kFC;
+    const int nf = min(kFC, F - f0);
+    for (int i = threadIdx.x; i < 2 * n_mels; i += blockDim.x) st_s[i] = stats[(int64_t)b * n_mels * 2 + i];
+    __syncthreads();
+    const float* tb = tmp + ((int64_t)b * F + f0) * n_mels;
+    float* dst = out + (int64_t)b * out_stride + (int64_t)(frame_off + f0) * n_mels;
+    for (int i = threadIdx.x; i < nf * n_mels; i += blockDim.x) {
+        const int m = i % n_mels;
+        const float x = tb[i];
+        dst[i] = normalize ? (x - st_s[2 * m]) / st_s[2 * m + 1] : x;
+    }
+}
+
 __global__ void pad_frames_kernel(const float* __restrict__ x, float* __restrict__ out, int out_frames, int off,
                                   int F, int C) {
     const int b = blockIdx.y;
@@ -134,6 +269,23 @@ VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t
     VASR_CHECK_ARG(out_stride >= (int64_t)(F + frame_off) * n_mels, "vasr_mel_log_norm_f32: out_stride too small");
     if (B == 0) return VASR_OK;
     hipStream_t s = as_stream(stream);
+    if (ld_power <= kMaxLdp && n_mels <= kMaxMels) {
+        // the chunked pair (the CSR goes to LDS when it has <= kMaxNnz entries: the 80 x 201
+        // HTK bank has 393)
+        const int nch = (F + kFC - 1) / kFC;
+        double* part = reinterpret_cast<double*>(workspace + (((int64_t)B * F * n_mels + 1) & ~(int64_t)1));
+        hipLaunchKernelGGL(mel_chunk_log_kernel, dim3(nch, B), dim3(256), 0, s, power, ld_power, stride_power,
+                           fb_rowptr, fb_col, fb_val, workspace, part, F, n_mels);
+        int rc = launch_status("vasr_mel_log_norm_f32/log");
+        if (rc) return rc;
+        float* stats = reinterpret_cast<float*>(part + (int64_t)B * nch * n_mels * 2);
+        hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(256), 0, s, part, stats, nch, F, n_mels, normalize);
+        rc = launch_status("vasr_mel_log_norm_f32/stats");
+        if (rc) return rc;
+        hipLaunchKernelGGL(mel_chunk_norm_kernel, dim3(nch, B), dim3(256), 0, s, workspace, stats, out, out_stride,
+                           frame_off, F, n_mels, normalize);
+        return launch_status("vasr_mel_log_norm_f32/norm");
+    }
     const int64_t total = (int64_t)B * F * n_mels;
     hipLaunchKernelGGL(mel_log_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, power, ld_power,
                        stride_power, fb_rowptr, fb_col, fb_val, workspace, B, F, n_mels);
@@ -144,7 +296,11 @@ VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t
     return launch_status("vasr_mel_log_norm_f32/norm");
 }
 
-VASR_API int64_t vasr_mel_workspace_floats(int B, int F, int n_mels) { return (int64_t)B * F * n_mels; }
+VASR_API int64_t vasr_mel_workspace_floats(int B, int F, int n_mels) {
+    const int64_t nch = (F + vasr::kFC - 1) / vasr::kFC;
+    // log-mel rows + fp64 (S, Q) partials per (chunk, bin) + {mean, denom} per bin
+    return (((int64_t)B * F * n_mels + 1) & ~(int64_t)1) + 4 * (int64_t)B * nch * n_mels + 2 * (int64_t)B * n_mels;
+}
 
 VASR_API int vasr_pad_frames_f32(const float* x, float* out, int out_frames, int off, int B, int F, int C,
                                  void* stream) {
