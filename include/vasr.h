@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 3
+#define VASR_ABI_VERSION 4
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -175,6 +175,14 @@ int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t stride_p
                           int normalize, float* workspace, void* stream);
 /* workspace size of vasr_mel_log_norm_f32 in floats (log-mel rows + per-chunk fp64 partials) */
 int64_t vasr_mel_workspace_floats(int B, int F, int n_mels);
+
+/* Steps 1 + 2 in one launch for n_fft = 400, hop = 160 (the reference defaults, audio.py:15-18):
+ * power[b][f][k] = |X_k|^2, k = 0..200, frame f of the reflect-padded audio (pad 200, computed
+ * on the fly, no padded copy) times window[0:400], by a 400-point real FFT in LDS (200-point
+ * complex FFT as 8 x 5 x 5 + real unpack).  F = S / 160 + 1 frames; power rows of stride ldp
+ * (>= 201), batch stride stride_power (>= F * ldp).  Needs S > 200 (torch's reflect-pad rule). */
+int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
+                            float* power, int64_t ldp, int64_t stride_power, void* stream);
 
 /* Write (B, F, C) rows into a zero-padded frame layout: out[b][off + f][c] = x[b][f][c]
  * and zero for the other out_frames - F frames (batch stride out_frames * C).  Feeds mel

@@ -258,7 +258,10 @@ def test_scan_gate_and_skip(va):
     ("short_400", lambda: S.make_audio(1, 400, seed=6)),
     ("oned_8000", lambda: S.make_audio(1, 8000, seed=9)[0]),
 ])
-def test_mel_matches_reference(va, name, make):
+@pytest.mark.parametrize("stft", ["fft", "gemm"])
+def test_mel_matches_reference(va, name, make, stft, monkeypatch):
+    from velocity_asr import audio as A
+    monkeypatch.setattr(A, "_STFT_FFT", stft == "fft")
     g = golden("mel.npz")
     audio = torch.from_numpy(make())
     mel = va.compute_mel_spectrogram(audio.to(DEV))
@@ -270,6 +273,38 @@ def test_mel_matches_reference(va, name, make):
     mel_cpu = va.compute_mel_spectrogram(audio)
     assert mel_cpu.device.type == "cpu"
     np.testing.assert_array_equal(mel_cpu.numpy(), mel.cpu().numpy())
+
+
+@pytest.mark.parametrize("S_", [201, 400, 1601, 16000, 16333, 160000])
+def test_stft_power_fft_vs_fp64(va, S_):
+    """Real-FFT power spectrogram vs torch.stft in fp64 (reference audio.py:97-115 in double):
+    |P - P64| <= 1e-5 * max(P64) per frame + 1e-6 relative (fp32 FFT rounding)."""
+    from velocity_asr import ops
+    x = S.make_audio(3, S_, seed=S_)
+    win = torch.hann_window(400)
+    p = ops.stft_power_400(t(x), win.to(DEV)).cpu().double()
+    xd = torch.from_numpy(x).double()
+    xp = torch.nn.functional.pad(xd.unsqueeze(1), (200, 200), mode="reflect").squeeze(1)
+    ref = torch.stft(xp, 400, 160, window=win.double(), center=False, return_complex=True).abs().pow(2).transpose(1, 2)
+    assert p.shape == ref.shape == (3, S_ // 160 + 1, 201)
+    frame_max = ref.amax(dim=2, keepdim=True)
+    err = (p - ref).abs() - 1e-6 * ref.abs()
+    assert (err <= 1e-5 * frame_max + 1e-12).all(), float((err / frame_max.clamp_min(1e-30)).max())
+
+
+def test_stft_power_fft_matches_dft_gemm(va):
+    """The FFT launch and the windowed-DFT GEMM (VASR_STFT=gemm) agree on the mel output."""
+    from velocity_asr import audio as A
+    x = t(S.make_audio(4, 160000, seed=77))
+    prev = A._STFT_FFT
+    try:
+        A._STFT_FFT = True
+        m_fft = A.mel_on_device(x)
+        A._STFT_FFT = False
+        m_gemm = A.mel_on_device(x)
+    finally:
+        A._STFT_FFT = prev
+    np.testing.assert_allclose(m_fft.cpu().numpy(), m_gemm.cpu().numpy(), atol=2e-4, rtol=1e-4)
 
 
 # ----------------------------------------------------------------------------- global context

@@ -1,8 +1,8 @@
 """Audio loading and the log-mel front end (drop-in for reference velocity_asr/audio.py).
 
-compute_mel_spectrogram runs on the MI355X: reflect pad (HIP) -> windowed-DFT GEMM with
-an in-register |X|^2 epilogue (fp32 MFMA) -> sparse mel + log + per-bin normalisation
-(HIP).  Input on the CPU is moved to the current HIP device and the result moved back,
+compute_mel_spectrogram runs on the MI355X: |STFT|^2 (HIP real FFT for the default n_fft 400 /
+hop 160 with reflect padding on the fly; otherwise reflect pad + a windowed-DFT GEMM with an
+in-register |X|^2 epilogue) -> sparse mel + log + per-bin normalisation (HIP).  Input on the CPU is moved to the current HIP device and the result moved back,
 so callers that compute mel on the host (scripts/transcribe.py:73) keep working; there is
 no CPU execution path.
 
@@ -167,6 +167,7 @@ class _FrontEndTables:
             W[64 * p + j] = win * np.cos(ang)
             W[64 * p + 32 + j] = -win * np.sin(ang)
         self.n_bins = n_bins
+        self.window = WINDOW_FN(n_fft).to(device)
         self.dft = torch.from_numpy(W.astype(np.float32)).to(device)
         fb = _create_mel_filterbank(n_fft, n_mels, sample_rate, torch.device("cpu"))
         nz = fb.nonzero(as_tuple=False)
@@ -216,6 +217,11 @@ def compute_mel_spectrogram(audio: torch.Tensor, sample_rate: int = SAMPLE_RATE,
     return mel.squeeze(0) if squeeze else mel
 
 
+# Default geometry (n_fft 400, hop 160): one real-FFT launch (vasr_stft_power_400_f32).  Other
+# geometries, or VASR_STFT=gemm: reflect pad + windowed-DFT GEMM with the |X|^2 epilogue.
+_STFT_FFT = os.environ.get("VASR_STFT", "fft") != "gemm"
+
+
 def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
                   hop_length: int = HOP_LENGTH, n_mels: int = N_MELS, normalize: bool = True) -> torch.Tensor:
     """(B, S) float32 HIP tensor -> (B, F, n_mels) on the same device."""
@@ -227,6 +233,9 @@ def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = 
         raise NotImplementedError("HIP front end needs n_fft and hop_length to be multiples of 4")
     n_frames = (S + 2 * pad - n_fft) // hop_length + 1
     tb = _tables(x.device, n_fft, n_mels, sample_rate)
+    if n_fft == 400 and hop_length == 160 and _STFT_FFT:
+        power = ops.stft_power_400(x, tb.window)
+        return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize)
     ld = (S + 2 * pad + 3) // 4 * 4
     xp = ops.reflect_pad(x, pad, ld)
     power = torch.empty((B, n_frames, tb.n_bins), device=x.device, dtype=torch.float32)

@@ -353,6 +353,21 @@ def reflect_pad(audio: torch.Tensor, pad: int, ld_out: int) -> torch.Tensor:
     return xp
 
 
+def stft_power_400(audio: torch.Tensor, window: torch.Tensor) -> torch.Tensor:
+    """(B, S) audio -> (B, S // 160 + 1, 201) |STFT|^2 (n_fft 400, hop 160, reflect pad, Hann)."""
+    _cuda_f32("stft_power_400.audio", audio)
+    _cuda_f32("stft_power_400.window", window)
+    audio = audio.contiguous()
+    B, S = audio.shape
+    if window.numel() != 400:
+        raise ValueError(f"stft_power_400: window must have 400 entries, got {window.numel()}")
+    F = S // 160 + 1
+    power = torch.empty((B, F, 201), device=audio.device, dtype=torch.float32)
+    check(L.lib().vasr_stft_power_400_f32(audio.data_ptr(), S, B, S, window.contiguous().data_ptr(), power.data_ptr(),
+                                          201, F * 201, stream_of(audio)), "vasr_stft_power_400_f32")
+    return power
+
+
 def mel_log_norm(power: torch.Tensor, ld_power: int, stride_power: int, fb_csr, B: int, F: int, n_mels: int,
                  normalize: bool) -> torch.Tensor:
     rowptr, col, val = fb_csr
