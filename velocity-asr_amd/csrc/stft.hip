@@ -1,9 +1,9 @@
 // Power spectrogram of the reference front end (audio.py:97-115: periodic Hann(400), reflect
 // pad 200, torch.stft n_fft 400 hop 160 center=False, |X|^2) as a real FFT, for n_fft = 400.
 //
-// Each workgroup takes 6 consecutive frames of one utterance: their 1200-sample span is read
-// once (reflect padding applied on the fly from the unpadded audio, no padded copy), windowed
-// and packed as z[n] = x[2n] + i x[2n+1] (a 200-point complex FFT of the even / odd samples),
+// Each workgroup takes 6 consecutive frames of one utterance, read straight from the unpadded
+// audio (reflect padding resolved per sample, no padded copy; overlapping frames hit in L2),
+// windowed and packed as z[n] = x[2n] + i x[2n+1] (a 200-point complex FFT of the even / odd samples),
 // transformed in LDS as 200 = 8 x (5 x 5) (Cooley-Tukey: 25 radix-8 DFTs with twiddles, then
 // two rounds of 40 radix-5 DFTs), and unpacked to the 201 bins of the real 400-point DFT:
 //   X[k] = (Z[k] + conj Z[200-k]) / 2 + W400^k (Z[k] - conj Z[200-k]) / (2i),  P[k] = |X[k]|^2.
@@ -28,7 +28,43 @@ __device__ __forceinline__ cf scale(cf a, float s) { return {a.x * s, a.y * s}; 
 
 constexpr int kNfft = 400, kHop = 160, kHalf = 200, kBins = 201;
 constexpr int kFPB = 6;                                // frames per workgroup
-constexpr int kSpan = (kFPB - 1) * kHop + kNfft;       // 1200 samples
+
+// Twiddle tables, evaluated at compile time in double (Taylor series about pi) and rounded once:
+// tw200[j] = W200^j = e^{-2 pi i j / 200}, tw400[k] = W400^k, k = 0..200.
+constexpr double kPi = 3.14159265358979323846;
+constexpr double taylor_sin(double y) {  // |y| <= pi
+    double term = y, sum = y;
+    for (int n = 1; n < 30; ++n) {
+        term *= -y * y / ((2.0 * n) * (2.0 * n + 1.0));
+        sum += term;
+    }
+    return sum;
+}
+constexpr double taylor_cos(double y) {
+    double term = 1.0, sum = 1.0;
+    for (int n = 1; n < 30; ++n) {
+        term *= -y * y / ((2.0 * n - 1.0) * (2.0 * n));
+        sum += term;
+    }
+    return sum;
+}
+struct TwTable {
+    cf w200[kHalf];
+    cf w400[kBins];
+};
+constexpr TwTable make_twiddles() {
+    TwTable t{};
+    for (int j = 0; j < kHalf; ++j) {
+        const double y = 2.0 * kPi * j / kHalf - kPi;  // e^{-i x} = (cos x, -sin x), x = y + pi
+        t.w200[j] = cf{(float)(-taylor_cos(y)), (float)(taylor_sin(y))};
+    }
+    for (int k = 0; k < kBins; ++k) {
+        const double y = 2.0 * kPi * k / kNfft - kPi;
+        t.w400[k] = cf{(float)(-taylor_cos(y)), (float)(taylor_sin(y))};
+    }
+    return t;
+}
+__constant__ constexpr TwTable kTw = make_twiddles();
 
 // Forward DFT-8 (radix-2, decimation in time), in place.
 __device__ __forceinline__ void dft8(cf (&v)[8]) {
@@ -70,41 +106,45 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
                                                              int S, int F, const float* __restrict__ window,
                                                              float* __restrict__ power, int64_t ldp,
                                                              int64_t stridep) {
-    __shared__ float samp[kSpan];
-    __shared__ float win[kNfft];
-    __shared__ cf tw200[kHalf];   // W200^j
-    __shared__ cf tw400[kBins];   // W400^k
+    __shared__ cf tw[kHalf + kBins];  // W200^j, then W400^k
     __shared__ cf za[kFPB][kHalf];
     __shared__ cf zb[kFPB][kHalf];
     const int b = blockIdx.y, f0 = blockIdx.x * kFPB;
     const int tid = threadIdx.x;
     const float* ab = audio + (int64_t)b * ld_audio;
-    // 1. span (reflect padding of n_fft / 2 on the fly), window, twiddles
-    const int pad = kNfft / 2;
-    for (int i = tid; i < kSpan; i += 256) {
-        int j = f0 * kHop + i - pad;
+    // 1. windowed even / odd sample pairs packed as complex, straight from the unpadded audio
+    //    (reflect padding of n_fft / 2 resolved per sample; the overlapping frames hit in L2).
+    //    Every global load of the block (twiddles, samples, window) is issued before the first
+    //    use, so the block waits for one memory latency, not one per loop trip.
+    constexpr int kTwIt = (kHalf + kBins + 255) / 256, kPackIt = (kFPB * kHalf + 255) / 256;
+    const float2* win2 = reinterpret_cast<const float2*>(window);
+    const cf* twg = reinterpret_cast<const cf*>(&kTw);  // w200 then w400, contiguous
+    cf twv[kTwIt];
+#pragma unroll
+    for (int it = 0; it < kTwIt; ++it) twv[it] = twg[min(tid + it * 256, kHalf + kBins - 1)];
+    auto reflect = [S](int j) {
         j = j < 0 ? -j : j;
         j = j >= S ? 2 * (S - 1) - j : j;
-        samp[i] = (j >= 0 && j < S) ? ab[j] : 0.f;  // frames past F read clamped data, never stored
-    }
-    for (int i = tid; i < kNfft; i += 256) win[i] = window[i];
-    for (int i = tid; i < kHalf + kBins; i += 256) {
-        float s, c;
-        if (i < kHalf) {
-            sincospif(2.0f * (float)i / (float)kHalf, &s, &c);
-            tw200[i] = cf{c, -s};
-        } else {
-            const int k = i - kHalf;
-            sincospif(2.0f * (float)k / (float)kNfft, &s, &c);
-            tw400[k] = cf{c, -s};
-        }
-    }
-    __syncthreads();
-    // 2. windowed even / odd samples packed as complex
-    for (int i = tid; i < kFPB * kHalf; i += 256) {
+        return min(max(j, 0), S - 1);  // frames past F read clamped data, never stored
+    };
+    float x0[kPackIt], x1[kPackIt];
+    float2 w[kPackIt];
+#pragma unroll
+    for (int it = 0; it < kPackIt; ++it) {
+        const int i = min(tid + it * 256, kFPB * kHalf - 1);
         const int q = i / kHalf, n = i - q * kHalf;
-        const float* fr = samp + q * kHop;
-        za[q][n] = cf{fr[2 * n] * win[2 * n], fr[2 * n + 1] * win[2 * n + 1]};
+        const int j0 = (f0 + q) * kHop + 2 * n - kNfft / 2;  // unpadded index of sample 2n
+        x0[it] = ab[reflect(j0)];
+        x1[it] = ab[reflect(j0 + 1)];
+        w[it] = win2[n];
+    }
+#pragma unroll
+    for (int it = 0; it < kTwIt; ++it)
+        if (tid + it * 256 < kHalf + kBins) tw[tid + it * 256] = twv[it];
+#pragma unroll
+    for (int it = 0; it < kPackIt; ++it) {
+        const int i = tid + it * 256;
+        if (i < kFPB * kHalf) (&za[0][0])[i] = cf{x0[it] * w[it].x, x1[it] * w[it].y};
     }
     __syncthreads();
     // 3. radix-8 over n1 (n = 25 n1 + n2), twiddle W200^(n2 k1); out [q][k1 * 25 + n2]
@@ -115,7 +155,7 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
         for (int n1 = 0; n1 < 8; ++n1) v[n1] = za[q][25 * n1 + n2];
         dft8(v);
 #pragma unroll
-        for (int k1 = 0; k1 < 8; ++k1) zb[q][k1 * 25 + n2] = k1 == 0 ? v[0] : cmul(v[k1], tw200[(n2 * k1) % kHalf]);
+        for (int k1 = 0; k1 < 8; ++k1) zb[q][k1 * 25 + n2] = k1 == 0 ? v[0] : cmul(v[k1], tw[(n2 * k1) % kHalf]);
     }
     __syncthreads();
     // 4. radix-5 over m1 (n2 = 5 m1 + m2), twiddle W25^(m2 j1) = W200^(8 m2 j1); out [q][k1*25 + m2*5 + j1]
@@ -127,7 +167,7 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
         dft5(v);
 #pragma unroll
         for (int j1 = 0; j1 < 5; ++j1)
-            za[q][k1 * 25 + m2 * 5 + j1] = j1 == 0 ? v[0] : cmul(v[j1], tw200[(8 * m2 * j1) % kHalf]);
+            za[q][k1 * 25 + m2 * 5 + j1] = j1 == 0 ? v[0] : cmul(v[j1], tw[(8 * m2 * j1) % kHalf]);
     }
     __syncthreads();
     // 5. radix-5 over m2 -> Z[k1 + 8 (j1 + 5 j2)] in natural order
@@ -141,19 +181,25 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
         for (int j2 = 0; j2 < 5; ++j2) zb[q][k1 + 8 * (j1 + 5 * j2)] = v[j2];
     }
     __syncthreads();
-    // 6. real-FFT unpack and power, coalesced rows
-    for (int i = tid; i < kFPB * kBins; i += 256) {
-        const int q = i / kBins, k = i - q * kBins;
-        const int f = f0 + q;
-        if (f >= F) continue;
-        const cf zk = zb[q][k % kHalf];
-        const cf zm = zb[q][(kHalf - k) % kHalf];
+    // 6. real-FFT unpack by bin pairs (k, 200 - k), k = 0..100: with A, B the even / odd spectra
+    //    at k, X[k] = A + W400^k B and X[200 - k] = conj(A - W400^k B).  |X|^2 is formed as
+    //    re^2 + im^2 (the reference rounds through abs(): at most 1 ulp apart).
+    float* pb = power + (int64_t)b * stridep + (int64_t)f0 * ldp;  // uniform base, 32-bit lane offsets
+    const int ldp32 = (int)ldp;
+#pragma unroll
+    for (int it = 0; it < (kFPB * 101 + 255) / 256; ++it) {
+        const int i = tid + it * 256;
+        const int q = i / 101, k = i - q * 101;
+        if (i >= kFPB * 101 || f0 + q >= F) continue;
+        const cf zk = zb[q][k];
+        const cf zm = zb[q][k == 0 ? 0 : kHalf - k];
         const cf zc = cf{zm.x, -zm.y};
         const cf A = scale(zk + zc, 0.5f);
-        const cf Bv = scale(mul_mi(zk - zc), 0.5f);
-        const cf X = A + cmul(tw400[k], Bv);
-        const float m = sqrtf(X.x * X.x + X.y * X.y);  // |X| squared, as abs()**2
-        power[(int64_t)b * stridep + (int64_t)f * ldp + k] = m * m;
+        const cf WB = cmul(tw[kHalf + k], scale(mul_mi(zk - zc), 0.5f));
+        const cf X1 = A + WB, X2 = A - WB;
+        float* row = pb + q * ldp32;
+        row[k] = X1.x * X1.x + X1.y * X1.y;
+        row[kHalf - k] = X2.x * X2.x + X2.y * X2.y;
     }
 }
 
@@ -164,6 +210,7 @@ VASR_API int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B
                                      float* power, int64_t ldp, int64_t stride_power, void* stream) {
     using namespace vasr;
     VASR_CHECK_ARG(audio && window && power, "vasr_stft_power_400_f32: null pointer");
+    VASR_CHECK_ARG(((uintptr_t)window & 7) == 0, "vasr_stft_power_400_f32: window must be 8-byte aligned");
     VASR_CHECK_ARG(B >= 0 && S > kNfft / 2 && ld_audio >= S && ldp >= kBins, "vasr_stft_power_400_f32: bad shape");
     const int F = (S + 2 * (kNfft / 2) - kNfft) / kHop + 1;
     VASR_CHECK_ARG(stride_power >= (int64_t)F * ldp, "vasr_stft_power_400_f32: stride_power too small");
