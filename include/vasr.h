@@ -99,6 +99,12 @@ int vasr_linear_f32(const vasr_gemm_args* args, void* stream);
  * (args->W is not read).  Replaces the same reference ops as vasr_linear_f32.
  */
 int vasr_linear_x3_f32(const vasr_gemm_args* args, const uint16_t* w_split, void* stream);
+/* Main-loop selection of vasr_linear_x3_f32 (same MFMA sequence, bit-identical results):
+ * 0 (default) = LDS-ring tiles; 1 / 2 (or env VASR_GEMM_PANEL=1 / 2) = LDS-resident 64-column
+ * weight panels with A streamed through registers at 4 / 2 waves per SIMD, used where
+ * K = 192 or 384 and the epilogue is unpaired (measured slower overall; experimental).
+ * Returns the previous setting; other values only query. */
+int vasr_set_x3_engine(int engine);
 
 /* Split W (N x K fp32, row stride ldw) into bf16 terms (hi, mid, lo) in the fragment-native
  * layout out[NT][KS][3][64][8] (NT = ceil(N/32), KS = Kp/16, Kp = K rounded up to 32):

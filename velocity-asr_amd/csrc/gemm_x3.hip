@@ -31,13 +31,12 @@
 #include <type_traits>
 
 #include "gemm_common.h"
+#include "gemm_split.h"
 
 namespace vasr {
 namespace {
 
 using namespace gemm;
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifndef VASR_X3_ABLATE
 #define VASR_X3_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no C stores, 4 no A split,
@@ -48,25 +47,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int BK = 32;  // fp32 k per stage (two MFMA k-steps)
 
 __device__ __forceinline__ int a_swz(int r) { return ((r >> 1) & 3) ^ (((r >> 3) & 1) << 2); }
-
-__device__ __forceinline__ void split1(float v, __bf16& hi, __bf16& mid, __bf16& lo) {
-    hi = (__bf16)v;
-    const float r1 = v - (float)hi;
-    mid = (__bf16)r1;
-    lo = (__bf16)(r1 - (float)mid);
-}
-
-__device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-    const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        __bf16 a, b, c;
-        split1(v[j], a, b, c);
-        hi[j] = a;
-        mid[j] = b;
-        lo[j] = c;
-    }
-}
 
 // LDS-DMA of 16 B per lane into dst_base + 16*lane, issued from inline asm: the compiler then
 // does not track it, so it adds no waits of its own before reads of other ring slots (its
@@ -471,6 +451,10 @@ VASR_API int vasr_linear_x3_f32(const vasr_gemm_args* a, const uint16_t* w_split
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     hipStream_t s = as_stream(stream);
+    if (epi != VASR_EPI_PAIR_POWER && epi != VASR_EPI_PAIR_FUSION) {
+        const int rc = try_panel_x3(p, epi, s);
+        if (rc <= 0) return rc;  // launched (or failed); 1: not eligible
+    }
 #ifdef VASR_X3_FORCE_CFG
     const int cfg = VASR_X3_FORCE_CFG;  // diagnostic builds only
 #else

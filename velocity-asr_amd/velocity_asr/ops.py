@@ -163,6 +163,17 @@ def pack_bf16(w: torch.Tensor) -> torch.Tensor:
     return packed
 
 
+def set_x3_engine(engine: str) -> str:
+    """Main loop of the split-bf16 GEMM: "tiles" (LDS-ring tiles, the default) or "panel" /
+    "panel2" (LDS-resident weight panels where the shape allows; experimental, bit-identical).
+    Returns the previous one."""
+    codes = {"tiles": 0, "panel": 1, "panel2": 2}  # panel2: the 2-waves-per-SIMD panel variant
+    if engine not in codes:
+        raise ValueError(f"x3 engine {engine!r}: expected one of {tuple(codes)}")
+    prev = L.lib().vasr_set_x3_engine(codes[engine])
+    return {v: k for k, v in codes.items()}[prev]
+
+
 def _linear(args: GemmArgs, w: torch.Tensor, stream) -> None:
     if w.dtype == torch.bfloat16:
         check(L.lib().vasr_linear_bf16(args, pack_bf16(w).data_ptr(), stream), "vasr_linear_bf16")
