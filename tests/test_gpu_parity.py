@@ -150,17 +150,21 @@ def test_split_weights_planes(va):
     assert (dense[:, N:, :] == 0).all() and (dense[:, :, K:] == 0).all()
 
 
-def test_layer_norm_and_dwconv(va):
+@pytest.mark.parametrize("L,C,Kc", [(37, 192, 4), (501, 192, 4), (16, 192, 4), (1, 192, 4), (3, 192, 4),
+                                    (37, 192, 3), (40, 96, 2), (33, 256, 7), (20, 64, 1)])
+def test_layer_norm_and_dwconv(va, L, C, Kc):
+    """LayerNorm and the fused LN + causal depthwise conv (Kc = 4 is the compile-time path,
+    other widths the generic one; full 16-row tiles, ragged last tiles, L < Kc)."""
     from velocity_asr import ops
-    rng = np.random.default_rng(0)
-    x = rng.standard_normal((2, 37, 192)).astype(np.float32) * 3 + 1
-    w = (1 + 0.1 * rng.standard_normal(192)).astype(np.float32)
-    b = (0.1 * rng.standard_normal(192)).astype(np.float32)
-    cw = rng.standard_normal((192, 1, 4)).astype(np.float32) * 0.3
-    cb = rng.standard_normal(192).astype(np.float32) * 0.1
+    rng = np.random.default_rng(L * 10 + Kc)
+    x = rng.standard_normal((2, L, C)).astype(np.float32) * 3 + 1
+    w = (1 + 0.1 * rng.standard_normal(C)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(C)).astype(np.float32)
+    cw = rng.standard_normal((C, 1, Kc)).astype(np.float32) * 0.3
+    cb = rng.standard_normal(C).astype(np.float32) * 0.1
     ln = ops.layer_norm(t(x), t(w), t(b)).cpu().numpy()
     np.testing.assert_allclose(ln, R.layer_norm(x, w, b), atol=2e-5, rtol=1e-5)
-    y = ops.ln_dwconv(t(x), t(w), t(b), t(cw.reshape(192, 4)), t(cb)).cpu().numpy()
+    y = ops.ln_dwconv(t(x), t(w), t(b), t(cw.reshape(C, Kc)), t(cb)).cpu().numpy()
     np.testing.assert_allclose(y, R.causal_dwconv(R.layer_norm(x, w, b), cw, cb), atol=3e-5, rtol=1e-5)
 
 

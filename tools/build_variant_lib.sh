@@ -1,0 +1,17 @@
+#!/bin/bash
+# Diagnostic: build the whole library with extra compile flags into tools/_variants/<name>.so,
+# for A/B timing through VASR_LIB=<path> (velocity_asr/_lib.py).
+#   tools/build_variant_lib.sh <name> [-DFLAG=...]...
+set -e
+NAME=$1; shift
+cd "$(dirname "$0")/../velocity-asr_amd"
+OUT=../tools/_variants/$NAME; mkdir -p "$OUT"
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -munsafe-fp-atomics $*"
+for f in csrc/*.hip csrc/*.cpp; do
+  extra=""; [ "$(basename $f)" = scan.hip ] && extra="-fno-slp-vectorize -ffp-contract=off"
+  /opt/rocm/bin/hipcc $FLAGS $extra -c "$f" -o "$OUT/$(basename $f).o" &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../tools/_variants/$NAME.so "$OUT"/*.o
+rm -rf "$OUT"
+echo ../tools/_variants/$NAME.so

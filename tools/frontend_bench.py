@@ -10,17 +10,27 @@ import torch  # noqa: E402
 from velocity_asr import _lib, audio as A, ops  # noqa: E402
 
 
-def timed(fn, iters=50):
-    for _ in range(5):
-        fn()
+def timed(fn, iters=20, reps=5):
+    """Per-call device time from a HIP graph of `iters` calls (no host launch overhead)."""
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(reps):
+        g.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) * 1e3 / iters
+    return a.elapsed_time(b) * 1e3 / (iters * reps)
 
 
 def main():

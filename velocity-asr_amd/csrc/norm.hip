@@ -48,20 +48,30 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
     ln_row_to(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
 }
 
-constexpr int TT = 16;       // output rows per block (1024 blocks at B=32, L=501: 4 per CU)
+#ifndef VASR_DW_TT
+#define VASR_DW_TT 16
+#endif
+constexpr int TT = VASR_DW_TT;  // output rows per block (1024 blocks at B=32, L=501: 4 per CU)
 constexpr int kMaxC = 256;   // LDS row capacity
 constexpr int kMaxK = 8;
 
 // Phase 1: the 4 waves layer-norm rows t0-(Kc-1) .. t0+TT-1 into LDS (zero rows before t=0).
 // Phase 2: thread c owns channel c for all TT rows: taps and bias in registers, a sliding
 // window of the last Kc LN values, one LDS read and one coalesced store per output.
+// KC: the conv width as a compile-time constant (the model's 4) so the taps, the window and
+// the history rows unroll without runtime guards; KC = 0 is the generic path (Kc <= kMaxK at
+// run time).  A runtime Kc turned every tap load and window read into its own guarded basic
+// block with a wait, serialising ~8 global-load latencies per thread (13.5 -> 4 us at B = 16).
+template <int KC>
 __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b,
                                                         const float* __restrict__ cw,
                                                         const float* __restrict__ cb, float* __restrict__ y,
-                                                        int L, int C, int Kc, float eps) {
-    __shared__ float tile[(TT + kMaxK - 1) * kMaxC];
+                                                        int L, int C, int Kc_rt, float eps) {
+    const int Kc = KC > 0 ? KC : Kc_rt;
+    constexpr int KM = KC > 0 ? KC : kMaxK;
+    __shared__ float tile[(TT + KM - 1) * kMaxC];
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * TT;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -69,7 +79,7 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     const float* xb = x + (int64_t)b * L * C;
     // Each wave normalises rows wave, wave + 4, ...: all of its row loads are issued before
     // the first reduction, so the rows' load latencies and butterfly chains overlap.
-    constexpr int RPW = (TT + kMaxK - 1 + 3) / 4;
+    constexpr int RPW = (TT + KM - 1 + 3) / 4;
     constexpr int CPL = kMaxC / 64;
     float v[RPW][CPL];
 #pragma unroll
@@ -117,24 +127,41 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     float* yb = y + (int64_t)b * L * C;
     const int rows = min(TT, L - t0);
     for (int c = threadIdx.x; c < C; c += 256) {
-        float w[kMaxK], win[kMaxK];
+        float w[KM], win[KM];
 #pragma unroll
-        for (int j = 0; j < kMaxK; ++j) {
-            w[j] = j < Kc ? cw[c * Kc + j] : 0.f;
+        for (int j = 0; j < KM; ++j) {
+            w[j] = (KC > 0 || j < Kc) ? cw[c * Kc + j] : 0.f;
             win[j] = (j < Kc - 1) ? tile[j * C + c] : 0.f;
         }
         const float bias = cb[c];
+        if (KC > 0 && rows == TT) {
+            // full tile: every LN row read up front, outputs in straight-line code
+            float lv[TT];
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt) lv[tt] = tile[(tt + KM - 1) * C + c];
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt) {
+                float acc = 0.f;
+#pragma unroll
+                for (int j = 0; j < KM; ++j) {
+                    const int r = tt + j - (KM - 1);  // LN row tt + j of the tile
+                    acc += (r < 0 ? win[j + tt] : lv[r]) * w[j];
+                }
+                yb[(int64_t)(t0 + tt) * C + c] = acc + bias;
+            }
+            continue;
+        }
         for (int tt = 0; tt < rows; ++tt) {
             // window = LN rows tt .. tt + Kc - 1 of the tile (inputs t - Kc + 1 .. t)
             const float v = tile[(tt + Kc - 1) * C + c];
             float acc = 0.f;
 #pragma unroll
-            for (int j = 0; j < kMaxK; ++j) {
+            for (int j = 0; j < KM; ++j) {
                 if (j < Kc - 1) acc += win[j] * w[j];
                 else if (j == Kc - 1) acc += v * w[j];
             }
 #pragma unroll
-            for (int j = 0; j + 1 < kMaxK; ++j) {
+            for (int j = 0; j + 1 < KM; ++j) {
                 if (j < Kc - 2) win[j] = win[j + 1];
                 else if (j == Kc - 2) win[j] = v;
             }
@@ -183,7 +210,11 @@ VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* 
     VASR_CHECK_ARG(C > 0 && C <= kMaxC && Kc >= 1 && Kc <= kMaxK && B >= 0 && L >= 0,
                    "vasr_ln_dwconv_f32: unsupported shape C=%d Kc=%d", C, Kc);
     if (B == 0 || L == 0) return VASR_OK;
-    hipLaunchKernelGGL(ln_dwconv_kernel, dim3((L + TT - 1) / TT, B), dim3(256), 0, as_stream(stream), x, ln_w,
-                       ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+    if (Kc == 4)
+        hipLaunchKernelGGL(ln_dwconv_kernel<4>, dim3((L + TT - 1) / TT, B), dim3(256), 0, as_stream(stream), x, ln_w,
+                           ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+    else
+        hipLaunchKernelGGL(ln_dwconv_kernel<0>, dim3((L + TT - 1) / TT, B), dim3(256), 0, as_stream(stream), x, ln_w,
+                           ln_b, conv_w, conv_b, y, L, C, Kc, eps);
     return launch_status("vasr_ln_dwconv_f32");
 }

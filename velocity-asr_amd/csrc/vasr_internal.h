@@ -30,10 +30,21 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 constexpr int kWave = 64;
 
+// Sum over the 64 lanes, broadcast to all: DPP within and across 16-lane rows (no LDS
+// round trips, unlike a ds_bpermute butterfly): row sums by quad_perm / half-mirror / mirror,
+// then row_bcast15 / row_bcast31 chain the rows into lane 63, read back as a scalar.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+    v += dpp_f<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f<0x141, 0xF>(v);  // row_half_mirror
+    v += dpp_f<0x140, 0xF>(v);  // row_mirror: every lane holds its row's sum
+    v += dpp_f<0x142, 0xA>(v);  // row_bcast15 -> rows 1, 3: r0+r1, r2+r3
+    v += dpp_f<0x143, 0xC>(v);  // row_bcast31 -> rows 2, 3: row 3 = r0+r1+r2+r3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {
