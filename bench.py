@@ -2,7 +2,7 @@
 """Throughput benchmark: VELOCITY-ASR inference, audio -> CTC tokens, on MI355X.
 
 Workload (BASELINE.json configs[1]): the 6.17 M-parameter fp32 model, batch of 32 synthetic
-10 s clips at 16 kHz per GPU.  One step = reflect pad + DFT-GEMM log-mel + full forward
+10 s clips at 16 kHz per GPU.  One step = real-FFT |STFT|^2 + log-mel + full forward
 (temporal binding, 8 SSM blocks, hierarchical global context, CTC head) + argmax + greedy
 collapse, on audio already resident in HBM, replayed as one HIP graph.  Multi-GPU: one
 process per GPU (torchrun), each rank transcribes its own 32 clips (utterance sharding, no

@@ -225,6 +225,21 @@ def test_scan_tree_vs_oracle_lengths(va, L):
     np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("npl", ["2", "4"])
+@pytest.mark.parametrize("N,L", [(16, 70), (32, 300), (64, 513)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_scan_lane_layouts(va, monkeypatch, npl, N, L, mode):
+    """Both lane layouts of the scan kernel (2 or 4 state indices per lane, VASR_SCAN_NPL)
+    against the oracle, tree (mode 0) and recurrence (mode 1); they differ only in the
+    order of the y = sum_n h C partial sums."""
+    monkeypatch.setenv("VASR_SCAN_NPL", npl)
+    x, dt, Bm, Cm, A_log, D = _scan_inputs(5 * N + L, 3, L, 64, N)
+    A = (-np.exp(A_log)).astype(np.float32)
+    ref = (R.parallel_scan if mode == 0 else R.sequential_scan)(x, dt, A, Bm, Cm, D)
+    got = _run_scan(x, dt, Bm, Cm, A_log, D, mode)
+    np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("N", [16, 32, 64])
 def test_scan_state_dims(va, N):
     x, dt, Bm, Cm, A_log, D = _scan_inputs(77 + N, 2, 70, 64, N)
