@@ -338,9 +338,10 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
     return VASR_OK;
 }
 
-// gemm_panel.hip: launches the LDS-resident-panel split GEMM when the shape suits it
-// (K = 192 / 384, unpaired epilogues); 1 when not eligible (the tile kernel runs instead).
-int try_panel_x3(const GemmParams& p, int epi, hipStream_t st);
+// gemm_panel.hip: launches the LDS-resident-panel split GEMM when it is enabled and the shape
+// suits it (K = 192 / 384, unpaired epilogues) and returns true with the launch status in *rc;
+// false when not eligible (the tile kernel runs instead).
+bool try_panel_x3(const GemmParams& p, int epi, hipStream_t st, int* rc);
 
 }  // namespace gemm
 }  // namespace vasr

@@ -317,7 +317,7 @@ int launch_panel(const GemmParams& p, int epi, hipStream_t st) {
         case VASR_EPI_RESIDUAL: VASR_P(VASR_EPI_RESIDUAL); break;
         case VASR_EPI_GELU_PE: VASR_P(VASR_EPI_GELU_PE); break;
         case VASR_EPI_ARGMAX: VASR_P(VASR_EPI_ARGMAX); break;
-        default: return 1;
+        default: set_error("vasr_linear_x3_f32 (panel): epilogue %d", epi); return VASR_EINVAL;
     }
 #undef VASR_P
     return launch_status("vasr_linear_x3_f32 (panel)");
@@ -329,22 +329,25 @@ int g_panel_enabled = -1;  // -1: from VASR_GEMM_PANEL (default 0: measured slow
 
 namespace gemm {
 
-int try_panel_x3(const GemmParams& p, int epi, hipStream_t st) {
+bool try_panel_x3(const GemmParams& p, int epi, hipStream_t st, int* rc) {
     if (g_panel_enabled < 0) {
         const char* e = std::getenv("VASR_GEMM_PANEL");
         g_panel_enabled = e ? std::atoi(e) : 0;
     }
-    if (!g_panel_enabled || p.K != p.Kp || p.K % 16 != 0) return 1;
+    if (!g_panel_enabled || p.K != p.Kp || p.K % 16 != 0) return false;
+    if (epi != VASR_EPI_NONE && epi != VASR_EPI_GELU && epi != VASR_EPI_SOFTPLUS_FROM && epi != VASR_EPI_RESIDUAL &&
+        epi != VASR_EPI_GELU_PE && epi != VASR_EPI_ARGMAX)
+        return false;
     const int ks = p.Kp / 16;
     if (g_panel_enabled == 2) {  // 2 waves per SIMD, deep ring, pipelined W reads
-        if (ks == 12) return launch_panel<12, 4, 2, 3, 4, true>(p, epi, st);
-        if (ks == 24) return launch_panel<24, 8, 1, 3, 4, true>(p, epi, st);
-        return 1;
+        if (ks == 12) return *rc = launch_panel<12, 4, 2, 3, 4, true>(p, epi, st), true;
+        if (ks == 24) return *rc = launch_panel<24, 8, 1, 3, 4, true>(p, epi, st), true;
+        return false;
     }
     // 4 waves per SIMD (16 per CU): 72 KiB panels x 2 blocks of 8 waves, or 144 KiB x 1 of 16
-    if (ks == 12) return launch_panel<12, 8, 2, 2, 2, false>(p, epi, st);
-    if (ks == 24) return launch_panel<24, 16, 1, 2, 2, false>(p, epi, st);
-    return 1;
+    if (ks == 12) return *rc = launch_panel<12, 8, 2, 2, 2, false>(p, epi, st), true;
+    if (ks == 24) return *rc = launch_panel<24, 16, 1, 2, 2, false>(p, epi, st), true;
+    return false;
 }
 
 }  // namespace gemm

@@ -452,8 +452,8 @@ VASR_API int vasr_linear_x3_f32(const vasr_gemm_args* a, const uint16_t* w_split
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     hipStream_t s = as_stream(stream);
     if (epi != VASR_EPI_PAIR_POWER && epi != VASR_EPI_PAIR_FUSION) {
-        const int rc = try_panel_x3(p, epi, s);
-        if (rc <= 0) return rc;  // launched (or failed); 1: not eligible
+        int rc;
+        if (try_panel_x3(p, epi, s, &rc)) return rc;
     }
 #ifdef VASR_X3_FORCE_CFG
     const int cfg = VASR_X3_FORCE_CFG;  // diagnostic builds only
