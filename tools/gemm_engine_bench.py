@@ -28,6 +28,7 @@ def timed(fn, iters=30):
 
 def main():
     _lib.require_device()
+    engines = ("tiles",) if sys.argv[1:] == ["tiles"] else ("tiles", "panel", "panel2")
     E = {"none": _lib.EPI_NONE, "softplus": _lib.EPI_SOFTPLUS_FROM, "residual": _lib.EPI_RESIDUAL, "gelu": _lib.EPI_GELU}
     for M in (8016, 16032):
         tot = {"tiles": 0.0, "panel": 0.0, "panel2": 0.0}
@@ -46,16 +47,15 @@ def main():
             else:
                 fn = lambda: ops.gemm(a, w, b, epilogue=E[epi], **kw)  # noqa: E731
             res = {}
-            for eng in ("tiles", "panel", "panel2"):
+            for eng in engines:
                 prev = ops.set_x3_engine(eng)
                 res[eng] = timed(fn)
                 ops.set_x3_engine(prev)
                 tot[eng] += res[eng]
             fl = 2.0 * M * N * K * 6
-            print(f"M={M:5d} {name:12s} N={N:4d} K={K}: tiles {res['tiles']:6.1f} us  panel {res['panel']:6.1f} us "
-                  f"({fl / res['panel'] / 1e6:.0f} bf16-TF/s)  panel2 {res['panel2']:6.1f} us", flush=True)
-        print(f"M={M:5d} per-SSM-block set (+head): tiles {tot['tiles']:.1f} us  panel {tot['panel']:.1f} us  "
-              f"panel2 {tot['panel2']:.1f} us")
+            print(f"M={M:5d} {name:12s} N={N:4d} K={K}: " + "  ".join(f"{e} {res[e]:6.1f} us" for e in engines)
+                  + f"  ({fl / res['tiles'] / 1e6:.0f} bf16-TF/s tiles)", flush=True)
+        print(f"M={M:5d} per-SSM-block set (+head): " + "  ".join(f"{e} {tot[e]:.1f} us" for e in engines))
 
 
 if __name__ == "__main__":
