@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 4
+#define VASR_ABI_VERSION 5
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -87,6 +87,15 @@ typedef struct vasr_gemm_args {
                                global_proj) followed by n_out entries for local_proj.
                                A column whose scale is 0 is not quantized.  Not allowed
                                with PAIR_POWER. */
+    /* ln_w / ln_b: NULL, or LayerNorm each A row over its K columns first:
+       A'[r][k] = (A[r][k] - mean_r) * rstd_r * ln_w[k] + ln_b[k], rstd_r = 1/sqrt(var_r + ln_eps)
+       (nn.LayerNorm(K) feeding the Linear: SSMBlock norm2 -> FFN, ssm.py:394-427; CTC head LN,
+       model.py:218-227).  The same float operations as vasr_layer_norm_f32, so the product
+       equals LN-then-GEMM bit for bit.  vasr_linear_x3_f32 / vasr_linear_bf16 only,
+       K % 32 == 0, K <= 384, epilogues NONE / GELU / RESIDUAL / ARGMAX. */
+    const float* ln_w;
+    const float* ln_b;
+    float ln_eps;
 } vasr_gemm_args;
 
 int vasr_linear_f32(const vasr_gemm_args* args, void* stream);

@@ -32,6 +32,9 @@ struct GemmParams {
     int n_out;
     const float4* qp;  // per-column activation fake-quant {scale, zp, qmin, qmax} or null
     int batch;
+    const float* ln_w;  // LayerNorm of each A row over K (weight, bias) before the product, or null
+    const float* ln_b;
+    float ln_eps;
 };
 
 struct Tile {
@@ -280,6 +283,7 @@ struct TileCfg {
     int bn() const { return wn * 32 * tn; }
 };
 constexpr int kCUs = 256;
+constexpr int kLnMaxK = 384;  // row-LayerNorm prologue: K (= the normalised width) limit
 
 // Pick the tile that minimises (rounds of resident blocks) x (blocks sharing a CU) x tile area:
 // at M = 16032 the grids are only one or two rounds deep, so wave quantisation and CU
@@ -335,6 +339,12 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
     p.aux2 = a->aux2; p.n_out = a->n_out;
     p.qp = reinterpret_cast<const float4*>(a->qparams);
     p.batch = a->batch;
+    p.ln_w = a->ln_w;
+    p.ln_b = a->ln_b;
+    p.ln_eps = a->ln_eps;
+    if (a->ln_w)
+        VASR_CHECK_ARG(a->ln_b != nullptr && a->K % 32 == 0 && a->K <= kLnMaxK,
+                       "%s: row LayerNorm needs ln_b, K %% 32 == 0 and K <= %d (K=%d)", fn, kLnMaxK, a->K);
     return VASR_OK;
 }
 

@@ -174,6 +174,7 @@ VASR_API int vasr_linear_f32(const vasr_gemm_args* a, void* stream) {
     using namespace vasr;
     GemmParams p;
     if (int rc = check_args(a, "vasr_linear_f32", p)) return rc;
+    VASR_CHECK_ARG(a->ln_w == nullptr, "vasr_linear_f32: the row-LayerNorm prologue is an x3 / bf16 engine feature");
     VASR_CHECK_ARG(a->W != nullptr, "vasr_linear_f32: null W");
     VASR_CHECK_ARG(a->ldw % 4 == 0 && (reinterpret_cast<uintptr_t>(a->W) & 15) == 0,
                    "vasr_linear_f32: W must be 16-byte aligned with ldw %% 4 == 0");

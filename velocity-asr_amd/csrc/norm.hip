@@ -35,7 +35,7 @@ __device__ __forceinline__ void ln_row_to(const float* __restrict__ x, const flo
 #pragma unroll
     for (int i = 0; i < kMaxPerLane; ++i) {
         const int c = i * 64 + lane;
-        if (c < C) y[c] = (v[i] - mean) * rstd * w[c] + b[c];
+        if (c < C) y[c] = __builtin_fmaf((v[i] - mean) * rstd, w[c], b[c]);  // as the GEMM LN prologue
     }
 }
 

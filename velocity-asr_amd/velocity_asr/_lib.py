@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -41,6 +41,7 @@ class GemmArgs(ctypes.Structure):
         ("aux2", c_p),
         ("n_out", c_i32),
         ("qparams", c_p),
+        ("ln_w", c_p), ("ln_b", c_p), ("ln_eps", ctypes.c_float),
     ]
 
 

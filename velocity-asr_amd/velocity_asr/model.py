@@ -122,8 +122,8 @@ class CTCOutputHead(nn.Module):
         B, L, D = x.shape
         ln = self.proj[0]
         w, b, qp = Q.linear_parts(self.proj[2])
-        h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
-        logits = ops.gemm(h.view(B * L, D), w, b, qparams=qp)
+        # the LayerNorm runs inside the GEMM's A read (identical float operations)
+        logits = ops.gemm(x.reshape(B * L, D), w, b, qparams=qp, ln=(ln.weight, ln.bias, ln.eps))
         Q.record(self.proj[2], logits)
         return logits.view(B, L, w.shape[0])
 
@@ -133,8 +133,7 @@ class CTCOutputHead(nn.Module):
         B, L, D = x.shape
         ln = self.proj[0]
         w, b, qp = Q.linear_parts(self.proj[2])
-        h = ops.layer_norm(x, ln.weight, ln.bias, ln.eps)
-        return ops.gemm_argmax(h.view(B * L, D), w, b, qparams=qp).view(B, L)
+        return ops.gemm_argmax(x.reshape(B * L, D), w, b, qparams=qp, ln=(ln.weight, ln.bias, ln.eps)).view(B, L)
 
 
 class VELOCITYASR(nn.Module):

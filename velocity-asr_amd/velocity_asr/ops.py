@@ -183,6 +183,30 @@ def _linear(args: GemmArgs, w: torch.Tensor, stream) -> None:
         check(L.lib().vasr_linear_f32(args, stream), "vasr_linear_f32")
 
 
+_LN_EPILOGUES = (L.EPI_NONE, L.EPI_GELU, L.EPI_RESIDUAL, L.EPI_ARGMAX)
+
+
+def _ln_prologue(a: torch.Tensor, w: torch.Tensor, ln, epilogue: int, args: GemmArgs):
+    """Row LayerNorm of `a`: by default vasr_layer_norm_f32 first; with VASR_LN_PROLOGUE=1 fused
+    into the GEMM's A read where the engine supports it (split-bf16 or bf16 engine, K % 32 == 0,
+    K <= 384, NONE / GELU / RESIDUAL / ARGMAX).  Both give identical results.  The fused form
+    is opt-in because it measured slower end to end (99.5k vs 102.5k RTFx): its per-block
+    statistics pass re-reads the A tile and delays the main loop by more than the separate
+    5-us LayerNorm launch costs, and the CTC head loses its 128 x 128 tile (LDS budget).
+    Returns the A the GEMM reads."""
+    if ln is None:
+        return a
+    ln_w, ln_b, eps = ln
+    ln_w, ln_b = f32(ln_w), f32(ln_b)
+    K = a.shape[1]
+    fused = ((w.dtype == torch.bfloat16 or _gemm_mode == "x3") and epilogue in _LN_EPILOGUES
+             and K % 32 == 0 and K <= 384 and os.environ.get("VASR_LN_PROLOGUE", "0") == "1")
+    if not fused:
+        return layer_norm(a, ln_w, ln_b, eps)
+    args.ln_w, args.ln_b, args.ln_eps = ln_w.data_ptr(), ln_b.data_ptr(), float(eps)
+    return a
+
+
 def _qp(qparams: Optional[torch.Tensor], cols: int) -> Optional[int]:
     if qparams is None:
         return None
@@ -195,10 +219,13 @@ def _qp(qparams: Optional[torch.Tensor], cols: int) -> Optional[int]:
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, epilogue: int = L.EPI_NONE,
          out: Optional[torch.Tensor] = None, aux: Optional[torch.Tensor] = None,
          aux2: Optional[torch.Tensor] = None, n_out: int = 0, n_cols_out: Optional[int] = None,
-         qparams: Optional[torch.Tensor] = None) -> torch.Tensor:
+         qparams: Optional[torch.Tensor] = None, ln=None) -> torch.Tensor:
     """out = epilogue(fq(a @ w.T + bias)) for a (M, K) row view and w (N, K); fq is the
-    per-column activation fake-quant of `qparams` ((ncols, 4) {scale, zp, qmin, qmax}) if given."""
+    per-column activation fake-quant of `qparams` ((ncols, 4) {scale, zp, qmin, qmax}) if given.
+    ln = (weight, bias, eps): LayerNorm each row of `a` first (fused into the A read)."""
     _cuda_f32("gemm.a", a)
+    args = GemmArgs()
+    a = _ln_prologue(a, w, ln, epilogue, args)
     _cuda_w("gemm.w", w)
     bias, aux, aux2 = f32(bias), f32(aux), f32(aux2)
     M, K, lda = _rows("gemm.a", a)
@@ -209,7 +236,6 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     if out is None:
         out = torch.empty((M, cols), device=a.device, dtype=torch.float32)
     _, _, ldc = _rows("gemm.out", out)
-    args = GemmArgs()
     args.A, args.lda, args.stride_a = a.data_ptr(), lda, 0
     args.W, args.ldw = w.data_ptr(), ldw
     args.bias = ptr(bias)
@@ -229,10 +255,13 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
 
 
 def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
-                qparams: Optional[torch.Tensor] = None) -> torch.Tensor:
+                qparams: Optional[torch.Tensor] = None, ln=None) -> torch.Tensor:
     """int32 argmax over the N outputs of a @ w.T + bias (after qparams) per row, fused into the
-    GEMM epilogue (VASR_EPI_ARGMAX): the (M, N) product is never written.  Ties -> first index."""
+    GEMM epilogue (VASR_EPI_ARGMAX): the (M, N) product is never written.  Ties -> first index.
+    ln = (weight, bias, eps): LayerNorm each row of `a` first (fused into the A read)."""
     _cuda_f32("gemm_argmax.a", a)
+    args = GemmArgs()
+    a = _ln_prologue(a, w, ln, L.EPI_ARGMAX, args)
     _cuda_w("gemm_argmax.w", w)
     bias = f32(bias)
     M, K, lda = _rows("gemm_argmax.a", a)
@@ -242,7 +271,6 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     slots = (N + 31) // 32
     keys = torch.empty((M, slots), device=a.device, dtype=torch.int64)  # every slot is written
     out = torch.empty(M, device=a.device, dtype=torch.int32)
-    args = GemmArgs()
     args.A, args.lda, args.stride_a = a.data_ptr(), lda, 0
     args.W, args.ldw = w.data_ptr(), ldw
     args.bias = ptr(bias)

@@ -123,8 +123,9 @@ class SSMBlock(nn.Module):
         g = self.ssm.gated_scan(u.view(B * L, D), B, L)
         x2 = x.view(B * L, D)
         x1 = ops.gemm(g, self.ssm.out_proj.weight, epilogue=_lib.EPI_RESIDUAL, aux=x2)
-        h = ops.layer_norm(x1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-        f = ops.gemm(h, self.ffn[0].weight, self.ffn[0].bias, epilogue=_lib.EPI_GELU)
+        # norm2 runs inside the FFN-in GEMM's A read (identical float operations)
+        f = ops.gemm(x1, self.ffn[0].weight, self.ffn[0].bias, epilogue=_lib.EPI_GELU,
+                     ln=(self.norm2.weight, self.norm2.bias, self.norm2.eps))
         out = ops.gemm(f, self.ffn[3].weight, self.ffn[3].bias, epilogue=_lib.EPI_RESIDUAL, aux=x1)
         return out.view(B, L, D)
 
