@@ -169,12 +169,17 @@ __global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restr
 
 // Per (b, bin): the chunk partials summed in a fixed order (3 interleaved phases, then the
 // phases in order) -> {mean, std + 1e-10} as floats.
-__global__ __launch_bounds__(256) void mel_chunk_stats_kernel(const double* __restrict__ part, float* __restrict__ stats,
-                                                              int nch, int F, int n_mels, int normalize) {
-    __shared__ double red[2][3][kMaxMels];
+// One workgroup per utterance; up to kStatPh phases of n_mels threads each sum a strided subset
+// of the chunk partials (4 accumulator pairs, loads in flight together), then the phases are
+// combined in a fixed order.  1024 threads: ~5 chunks per thread at F = 1001, so the kernel is
+// two memory round trips long instead of six (10.4 -> see DESIGN).
+constexpr int kStatPh = 12;
+__global__ __launch_bounds__(1024) void mel_chunk_stats_kernel(const double* __restrict__ part, float* __restrict__ stats,
+                                                               int nch, int F, int n_mels, int normalize) {
+    __shared__ double red[2][kStatPh][kMaxMels];
     const int b = blockIdx.x;
-    const int m = threadIdx.x % n_mels, ph = threadIdx.x / n_mels;  // 3 phases of n_mels threads (n_mels <= 85)
-    const int nph = min(3, (int)blockDim.x / n_mels);
+    const int m = threadIdx.x % n_mels, ph = threadIdx.x / n_mels;  // phases of n_mels threads (n_mels <= 85)
+    const int nph = min(kStatPh, (int)blockDim.x / n_mels);
     if (ph < nph) {
         // four independent accumulator pairs (loads in flight together), combined in a fixed order
         double S[4] = {0.0, 0.0, 0.0, 0.0}, Q[4] = {0.0, 0.0, 0.0, 0.0};
@@ -279,7 +284,7 @@ VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t
         int rc = launch_status("vasr_mel_log_norm_f32/log");
         if (rc) return rc;
         float* stats = reinterpret_cast<float*>(part + (int64_t)B * nch * n_mels * 2);
-        hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(256), 0, s, part, stats, nch, F, n_mels, normalize);
+        hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(1024), 0, s, part, stats, nch, F, n_mels, normalize);
         rc = launch_status("vasr_mel_log_norm_f32/stats");
         if (rc) return rc;
         hipLaunchKernelGGL(mel_chunk_norm_kernel, dim3(nch, B), dim3(256), 0, s, workspace, stats, out, out_stride,
