@@ -198,6 +198,16 @@ int64_t vasr_mel_workspace_floats(int B, int F, int n_mels);
  * (>= 201), batch stride stride_power (>= F * ldp).  Needs S > 200 (torch's reflect-pad rule). */
 int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
                             float* power, int64_t ldp, int64_t stride_power, void* stream);
+/* The whole front end for n_fft = 400, hop = 160 with the power spectrum kept on chip: the
+ * real FFT above for one 16-frame chunk per workgroup, then in the same workgroup mel + log
+ * of the chunk and its per-bin fp64 partials, then the stats / normalisation passes of
+ * vasr_mel_log_norm_f32 (same workspace, same outputs bit for bit as stft_power + mel_log_norm).
+ * n_mels <= 85; out / out_stride / frame_off / normalize as in vasr_mel_log_norm_f32.
+ * Measured slower than the two-step form (39.9 vs 35.4 us for 16 x 10 s): opt-in. */
+int vasr_stft_logmel_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
+                             const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
+                             float* out, int64_t out_stride, int frame_off, int n_mels, int normalize,
+                             float* workspace, void* stream);
 
 /* Write (B, F, C) rows into a zero-padded frame layout: out[b][off + f][c] = x[b][f][c]
  * and zero for the other out_frames - F frames (batch stride out_frames * C).  Feeds mel

@@ -277,10 +277,11 @@ def test_scan_gate_and_skip(va):
     ("short_400", lambda: S.make_audio(1, 400, seed=6)),
     ("oned_8000", lambda: S.make_audio(1, 8000, seed=9)[0]),
 ])
-@pytest.mark.parametrize("stft", ["fft", "gemm"])
+@pytest.mark.parametrize("stft", ["fft", "fused", "gemm"])
 def test_mel_matches_reference(va, name, make, stft, monkeypatch):
     from velocity_asr import audio as A
-    monkeypatch.setattr(A, "_STFT_FFT", stft == "fft")
+    monkeypatch.setattr(A, "_STFT_FFT", stft != "gemm")
+    monkeypatch.setattr(A, "_STFT_MODE", stft)
     g = golden("mel.npz")
     audio = torch.from_numpy(make())
     mel = va.compute_mel_spectrogram(audio.to(DEV))
@@ -311,19 +312,19 @@ def test_stft_power_fft_vs_fp64(va, S_):
     assert (err <= 1e-5 * frame_max + 1e-12).all(), float((err / frame_max.clamp_min(1e-30)).max())
 
 
-def test_stft_power_fft_matches_dft_gemm(va):
-    """The FFT launch and the windowed-DFT GEMM (VASR_STFT=gemm) agree on the mel output."""
+@pytest.mark.parametrize("S_", [160000, 201, 16333, 2559])
+def test_stft_power_fft_matches_dft_gemm(va, monkeypatch, S_):
+    """The fused FFT + log-mel launch equals the FFT launch + log-mel passes bit for bit (same
+    float operations), and both agree with the windowed-DFT GEMM (VASR_STFT=gemm) on the mel."""
     from velocity_asr import audio as A
-    x = t(S.make_audio(4, 160000, seed=77))
-    prev = A._STFT_FFT
-    try:
-        A._STFT_FFT = True
-        m_fft = A.mel_on_device(x)
-        A._STFT_FFT = False
-        m_gemm = A.mel_on_device(x)
-    finally:
-        A._STFT_FFT = prev
-    np.testing.assert_allclose(m_fft.cpu().numpy(), m_gemm.cpu().numpy(), atol=2e-4, rtol=1e-4)
+    x = t(S.make_audio(4, S_, seed=77))
+    out = {}
+    for mode in ("fft", "fused", "gemm"):
+        monkeypatch.setattr(A, "_STFT_FFT", mode != "gemm")
+        monkeypatch.setattr(A, "_STFT_MODE", mode)
+        out[mode] = A.mel_on_device(x).cpu()
+    assert torch.equal(out["fft"], out["fused"])
+    np.testing.assert_allclose(out["fft"].numpy(), out["gemm"].numpy(), atol=2e-4, rtol=1e-4)
 
 
 # ----------------------------------------------------------------------------- global context

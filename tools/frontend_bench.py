@@ -57,10 +57,14 @@ def main():
     def mel():
         ops.mel_log_norm(p, 201, F * 201, tb.fb_csr, B, F, 80, True)
 
-    t_fft, t_gemm, t_mel = timed(fft), timed(gemm), timed(mel)
+    def fused():
+        ops.stft_logmel_400(x, tb.window, tb.fb_csr, 80, True)
+
+    t_fft, t_gemm, t_mel, t_fused = timed(fft), timed(gemm), timed(mel), timed(fused)
     byt = B * S * 4 + B * F * 201 * 4
     print(f"B={B} S={S} F={F}: stft fft {t_fft:.1f} us ({byt / t_fft / 1e3:.0f} GB/s algorithmic), "
-          f"pad+dft gemm {t_gemm:.1f} us, log-mel+norm {t_mel:.1f} us")
+          f"pad+dft gemm {t_gemm:.1f} us, log-mel+norm {t_mel:.1f} us; fused fft+log-mel+norm {t_fused:.1f} us "
+          f"(vs {t_fft + t_mel:.1f} us in two steps)")
 
 
 if __name__ == "__main__":

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void mel_norm_kernel(const float* __restrict__
 //  B (mel_chunk_norm_kernel): per bin, the chunk partials summed in chunk order (deterministic):
 //    mean = S / F, unbiased var = (Q - S mean) / (F - 1) in fp64 (exact mean for constant rows,
 //    so silent audio still gives 0), then the chunk's normalised rows.
-constexpr int kFC = 16;
+constexpr int kFC = kMelChunk;  // frames per chunk (vasr_internal.h)
 constexpr int kMaxLdp = 256;
 constexpr int kMaxNnz = 1024;
 constexpr int kMaxMels = 85;  // 3 bins-wide phases of a 256-thread block
@@ -248,6 +248,22 @@ __global__ void pad_frames_kernel(const float* __restrict__ x, float* __restrict
 }
 
 }  // namespace
+
+// Stats + normalisation passes of the chunked front end over the workspace written by a
+// chunk-log pass (mel_chunk_log_kernel, or the fused STFT + log-mel of stft.hip).
+int mel_chunk_finish(float* workspace, float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
+                     int normalize, hipStream_t s) {
+    const int nch = (F + kFC - 1) / kFC;
+    double* part = reinterpret_cast<double*>(workspace + (((int64_t)B * F * n_mels + 1) & ~(int64_t)1));
+    float* stats = reinterpret_cast<float*>(part + (int64_t)B * nch * n_mels * 2);
+    hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(1024), 0, s, part, stats, nch, F, n_mels, normalize);
+    int rc = launch_status("mel stats");
+    if (rc) return rc;
+    hipLaunchKernelGGL(mel_chunk_norm_kernel, dim3(nch, B), dim3(256), 0, s, workspace, stats, out, out_stride,
+                       frame_off, F, n_mels, normalize);
+    return launch_status("mel norm");
+}
+
 }  // namespace vasr
 
 VASR_API int vasr_reflect_pad_f32(const float* audio, int64_t ld_audio, float* xp, int64_t ld_out, int B, int S,
@@ -283,13 +299,7 @@ VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t
                            fb_rowptr, fb_col, fb_val, workspace, part, F, n_mels);
         int rc = launch_status("vasr_mel_log_norm_f32/log");
         if (rc) return rc;
-        float* stats = reinterpret_cast<float*>(part + (int64_t)B * nch * n_mels * 2);
-        hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(1024), 0, s, part, stats, nch, F, n_mels, normalize);
-        rc = launch_status("vasr_mel_log_norm_f32/stats");
-        if (rc) return rc;
-        hipLaunchKernelGGL(mel_chunk_norm_kernel, dim3(nch, B), dim3(256), 0, s, workspace, stats, out, out_stride,
-                           frame_off, F, n_mels, normalize);
-        return launch_status("vasr_mel_log_norm_f32/norm");
+        return mel_chunk_finish(workspace, out, out_stride, frame_off, B, F, n_mels, normalize, s);
     }
     const int64_t total = (int64_t)B * F * n_mels;
     hipLaunchKernelGGL(mel_log_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, power, ld_power,

@@ -28,6 +28,12 @@ inline int launch_status(const char* what) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// mel.hip: the stats + normalisation passes of the chunked log-mel front end (kFC = 16 frames
+// per chunk) over a workspace laid out as vasr_mel_workspace_floats describes.
+constexpr int kMelChunk = 16;
+int mel_chunk_finish(float* workspace, float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
+                     int normalize, hipStream_t s);
+
 constexpr int kWave = 64;
 
 // Sum over the 64 lanes, broadcast to all: DPP within and across 16-lane rows (no LDS

@@ -65,6 +65,8 @@ _SIGNATURES = {
                               ctypes.c_int),
     "vasr_mel_workspace_floats": ([ctypes.c_int] * 3, c_i64),
     "vasr_set_x3_engine": ([ctypes.c_int], ctypes.c_int),
+    "vasr_stft_logmel_400_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 3
+                                 + [c_p, c_p], ctypes.c_int),
     "vasr_stft_power_400_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_i64, c_i64, c_p], ctypes.c_int),
     "vasr_pad_frames_f32": ([c_p, c_p] + [ctypes.c_int] * 5 + [c_p], ctypes.c_int),
     "vasr_adaptive_pool_f32": ([c_p, c_p] + [ctypes.c_int] * 4 + [c_p], ctypes.c_int),

@@ -217,9 +217,14 @@ def compute_mel_spectrogram(audio: torch.Tensor, sample_rate: int = SAMPLE_RATE,
     return mel.squeeze(0) if squeeze else mel
 
 
-# Default geometry (n_fft 400, hop 160): one real-FFT launch (vasr_stft_power_400_f32).  Other
-# geometries, or VASR_STFT=gemm: reflect pad + windowed-DFT GEMM with the |X|^2 epilogue.
-_STFT_FFT = os.environ.get("VASR_STFT", "fft") != "gemm"
+# Default geometry (n_fft 400, hop 160): the real-FFT launch writing |X|^2 rows (6 frames per
+# workgroup), then the chunked log-mel passes.  VASR_STFT=fused: FFT + log-mel chunk pass in one
+# launch (vasr_stft_logmel_400_f32, 16 frames per workgroup, power kept in LDS; bit-identical,
+# but measured slower: 39.9 vs 35.4 us per 16-clip launch, the larger workgroups hide less
+# latency).  VASR_STFT=gemm or other geometries: reflect pad + windowed-DFT GEMM with the |X|^2
+# epilogue.
+_STFT_MODE = os.environ.get("VASR_STFT", "fft")
+_STFT_FFT = _STFT_MODE != "gemm"
 
 
 def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
@@ -234,6 +239,8 @@ def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = 
     n_frames = (S + 2 * pad - n_fft) // hop_length + 1
     tb = _tables(x.device, n_fft, n_mels, sample_rate)
     if n_fft == 400 and hop_length == 160 and _STFT_FFT:
+        if _STFT_MODE == "fused" and n_mels <= 85:  # FFT + log-mel in one launch (power stays in LDS)
+            return ops.stft_logmel_400(x, tb.window, tb.fb_csr, n_mels, normalize)
         power = ops.stft_power_400(x, tb.window)
         return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize)
     ld = (S + 2 * pad + 3) // 4 * 4

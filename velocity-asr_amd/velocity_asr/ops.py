@@ -407,6 +407,23 @@ def stft_power_400(audio: torch.Tensor, window: torch.Tensor) -> torch.Tensor:
     return power
 
 
+def stft_logmel_400(audio: torch.Tensor, window: torch.Tensor, fb_csr, n_mels: int, normalize: bool) -> torch.Tensor:
+    """(B, S) audio -> (B, S // 160 + 1, n_mels) normalised log-mel (n_fft 400, hop 160): one fused
+    FFT + log-mel launch (power stays on chip) and the stats / normalisation passes."""
+    _cuda_f32("stft_logmel_400.audio", audio)
+    _cuda_f32("stft_logmel_400.window", window)
+    audio = audio.contiguous()
+    B, S = audio.shape
+    F = S // 160 + 1
+    rowptr, col, val = fb_csr
+    out = torch.empty((B, F, n_mels), device=audio.device, dtype=torch.float32)
+    ws = torch.empty(int(L.lib().vasr_mel_workspace_floats(B, F, n_mels)), device=audio.device, dtype=torch.float32)
+    check(L.lib().vasr_stft_logmel_400_f32(audio.data_ptr(), S, B, S, window.contiguous().data_ptr(), rowptr.data_ptr(),
+                                           col.data_ptr(), val.data_ptr(), out.data_ptr(), F * n_mels, 0, n_mels,
+                                           int(normalize), ws.data_ptr(), stream_of(audio)), "vasr_stft_logmel_400_f32")
+    return out
+
+
 def mel_log_norm(power: torch.Tensor, ld_power: int, stride_power: int, fb_csr, B: int, F: int, n_mels: int,
                  normalize: bool) -> torch.Tensor:
     rowptr, col, val = fb_csr
