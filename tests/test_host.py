@@ -40,6 +40,17 @@ def test_abi_rejects_bad_arguments_without_gpu():
     assert L.vasr_linear_x3_f32(ctypes.byref(args), None, None) == -1
     assert L.vasr_split_weights_bf16x3(None, 4, 4, 4, None, None) == -1
     assert L.vasr_split_weights_elems(70, 100) == 3 * 96 * 128
+    # front end: null pointers and too-short audio are rejected before any launch
+    assert L.vasr_stft_power_400_f32(None, 0, 1, 1000, None, None, 201, 201, None) == -1
+    assert L.vasr_stft_logmel_400_f32(None, 0, 1, 1000, None, None, None, None, None, 0, 0, 80, 1, None, None) == -1
+    # the row-LayerNorm prologue is refused by the f32 engine and needs K % 32 == 0
+    args = _lib.GemmArgs()
+    args.A = args.C = args.W = args.ln_w = args.ln_b = 16
+    args.batch, args.M, args.N, args.K, args.lda, args.ldw, args.ldc = 1, 4, 4, 36, 36, 36, 4
+    assert L.vasr_linear_f32(ctypes.byref(args), None) == -1
+    assert b"LayerNorm" in L.vasr_last_error()
+    # engine switch: query only (values outside 0..2 change nothing)
+    assert L.vasr_set_x3_engine(-1) == L.vasr_set_x3_engine(-1)
 
 
 def test_public_api_matches_reference_all():
