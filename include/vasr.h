@@ -161,6 +161,9 @@ int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b,
  *          float-operation order with an O(log L) block stack per state lane;
  *   mode 1 (scan_mode="sequential"): the true recurrence h_t = dA_t h_{t-1} + dBx_t
  *          (ssm.py:134-171);
+ *   mode 2: the tree of mode 0 with each a*b + c as one fused multiply-add and
+ *          dBx = (x*dt)*B (one rounding fewer per op; the model's default for
+ *          scan_mode="parallel", VASR_SCAN_FMA=0 selects mode 0);
  *   out[b,t,d] = (sum_n h[b,t,d,n] C[b,t,n] + x[b,t,d] D[d]) * silu(z[b,t,d]).
  * x = xz[:, :, 0:Di], z = xz[:, :, Di:2Di]; B = bc[:, :, 0:N], C = bc[:, :, N:2N].
  * A2 = A * log2(e) (A = -exp(A_log), shared across Di).  N in {16, 32, 64};

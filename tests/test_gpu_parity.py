@@ -212,22 +212,26 @@ def test_scan_matches_reference_golden(va, case):
     x, dt, Bm, Cm, A_log, D = _scan_inputs(seed, B, L, Di, N)
     yp = _run_scan(x, dt, Bm, Cm, A_log, D, 0)
     ys = _run_scan(x, dt, Bm, Cm, A_log, D, 1)
+    yf = _run_scan(x, dt, Bm, Cm, A_log, D, 2)
     np.testing.assert_allclose(yp, g[name + "__parallel"], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(yf, g[name + "__parallel"], atol=1e-4, rtol=1e-4)
     np.testing.assert_allclose(ys, g[name + "__sequential"], atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("L", [1, 2, 15, 16, 17, 33, 255, 256, 257, 511, 512, 513, 1024, 2049])
-def test_scan_tree_vs_oracle_lengths(va, L):
+def test_scan_tree_vs_oracle_lengths(va, L, mode):
+    """The tree scan op for op (mode 0) and with fused multiply-adds (mode 2) vs the oracle."""
     x, dt, Bm, Cm, A_log, D = _scan_inputs(1000 + L, 1, L, 16, 64)
     A = (-np.exp(A_log)).astype(np.float32)
     ref = R.parallel_scan(x, dt, A, Bm, Cm, D)
-    got = _run_scan(x, dt, Bm, Cm, A_log, D, 0)
+    got = _run_scan(x, dt, Bm, Cm, A_log, D, mode)
     np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-4)
 
 
 @pytest.mark.parametrize("npl", ["2", "4"])
 @pytest.mark.parametrize("N,L", [(16, 70), (32, 300), (64, 513)])
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_scan_lane_layouts(va, monkeypatch, npl, N, L, mode):
     """Both lane layouts of the scan kernel (2 or 4 state indices per lane, VASR_SCAN_NPL)
     against the oracle, tree (mode 0) and recurrence (mode 1); they differ only in the
@@ -235,7 +239,7 @@ def test_scan_lane_layouts(va, monkeypatch, npl, N, L, mode):
     monkeypatch.setenv("VASR_SCAN_NPL", npl)
     x, dt, Bm, Cm, A_log, D = _scan_inputs(5 * N + L, 3, L, 64, N)
     A = (-np.exp(A_log)).astype(np.float32)
-    ref = (R.parallel_scan if mode == 0 else R.sequential_scan)(x, dt, A, Bm, Cm, D)
+    ref = (R.sequential_scan if mode == 1 else R.parallel_scan)(x, dt, A, Bm, Cm, D)
     got = _run_scan(x, dt, Bm, Cm, A_log, D, mode)
     np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-4)
 

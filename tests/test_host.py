@@ -33,6 +33,10 @@ def test_abi_rejects_bad_arguments_without_gpu():
     L = _lib.load()
     rc = L.vasr_ssm_scan_f32(None, 0, None, 0, None, 0, None, None, None, 0, 1, 1, 384, 64, 0, None)
     assert rc == -1 and b"null" in L.vasr_last_error()
+    # modes 0 (tree), 1 (recurrence), 2 (tree with fused multiply-adds); anything else is refused
+    fake = 256  # aligned non-null pointer values: the checks return before any dereference
+    rc = L.vasr_ssm_scan_f32(fake, 768, fake, 384, fake, 128, fake, fake, fake, 384, 1, 1, 384, 64, 3, None)
+    assert rc == -1 and b"mode" in L.vasr_last_error()
     rc = L.vasr_ctc_collapse(None, 1, 1, 0, 1, None, None, None, None, None)
     assert rc == -1
     args = _lib.GemmArgs()

@@ -1,0 +1,100 @@
+"""Whole-model parity of both tree-scan kernel modes against the reference goldens
+(pytest -m gpu): mode 2 (fused multiply-adds, the default) and mode 0 (VASR_SCAN_FMA=0).
+
+Mode 2 evaluates the same exclusive, mis-combined Blelloch tree as the reference's
+_associative_scan (ssm.py:216-295) but rounds each a*b + c once (v_pk_fma_f32) and forms
+x*dt before scaling B (ssm.py:198-202 form x*(dt*B)), so it is no longer op-for-op equal
+to the reference; the bar is the fp32 one of the whole suite:
+  * logits vs reference golden: atol 5e-4, rtol 1e-4
+  * CTC argmax tokens and greedy token lists: bit-exact
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_json
+from velocity_asr import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+LOGIT_TOL = dict(atol=5e-4, rtol=1e-4)
+
+
+@pytest.fixture(scope="module")
+def va():
+    import velocity_asr
+    from velocity_asr import _lib
+    _lib.require_device()
+    _lib.load()
+    return velocity_asr
+
+
+@pytest.fixture(scope="module")
+def model(va):
+    m = va.VELOCITYASR(va.VelocityASRConfig())
+    W = S.make_weights(None, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    return m.to(DEV).eval()
+
+
+@pytest.fixture(params=["0", "1"])
+def fma(request, monkeypatch):
+    monkeypatch.setenv("VASR_SCAN_FMA", request.param)
+    return request.param
+
+
+def t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+
+
+def test_fma_headline_shape_b2_10s(va, model, fma):
+    g = golden("fwd_b2_10s.npz")
+    logits = model(va.compute_mel_spectrogram(t(S.make_audio(2, 160000, seed=1234))))
+    np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
+    np.testing.assert_allclose(logits[:, g["frames"]].cpu().numpy(), g["logits_sub"], **LOGIT_TOL)
+    assert va.ctc_greedy_decode(logits) == golden_json("decode_fwd.json")["results"]["b2_10s"]
+
+
+def test_fma_b2_3s_and_stages(va, model, fma):
+    g = golden("fwd_b2_3s.npz")
+    logits, f = model(t(g["mel"]), return_features=True)
+    np.testing.assert_allclose(f["local_features"].cpu().numpy(), g["local_features"], atol=3e-4, rtol=1e-4)
+    np.testing.assert_allclose(logits.cpu().numpy(), g["logits"], **LOGIT_TOL)
+    np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
+
+
+def test_fma_long_utterance_30s(va, model, fma):
+    g = golden("fwd_b1_30s.npz")
+    logits = model(va.compute_mel_spectrogram(t(S.make_audio(1, 480000, seed=4321))))
+    np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
+    np.testing.assert_allclose(logits[:, g["frames"]].cpu().numpy(), g["logits_sub"], **LOGIT_TOL)
+
+
+def test_fma_edge_lengths_and_chirp(va, model, fma):
+    g = golden("fwd_edge.npz")
+    for S_, seed in ((201, 31), (400, 32), (1600, 33), (8000, 34), (16333, 35)):
+        logits = model(va.compute_mel_spectrogram(t(S.make_audio(1, S_, seed=seed))))
+        np.testing.assert_allclose(logits.cpu().numpy(), g[f"S{S_}__logits"], **LOGIT_TOL)
+        np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g[f"S{S_}__tokens"])
+    g = golden("fwd_chirp_3s.npz")
+    logits = model(va.compute_mel_spectrogram(t(S.make_chirp(48000)[None])))
+    np.testing.assert_allclose(logits.cpu().numpy(), g["logits"], **LOGIT_TOL)
+    np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
+
+
+def test_fma_full_batch_32x10s(va, model, fma):
+    """The bench shape: deterministic, golden clips' tokens, and mode 2 tokens equal to mode 0."""
+    import os
+    mel = va.compute_mel_spectrogram(t(S.make_audio(32, 160000, seed=1234)))
+    l1 = model(mel)
+    assert torch.equal(l1, model(mel))
+    g = golden("fwd_b2_10s.npz")
+    np.testing.assert_array_equal(l1[:2].argmax(-1).cpu().numpy(), g["tokens"])
+    os.environ["VASR_SCAN_FMA"] = "0" if fma == "1" else "1"
+    l0 = model(mel)
+    os.environ["VASR_SCAN_FMA"] = fma
+    agree = (l0.argmax(-1) == l1.argmax(-1)).float().mean().item()
+    assert agree == 1.0, f"argmax agreement between scan modes {agree}"
+    assert (l0 - l1).abs().max().item() < 5e-4

@@ -16,6 +16,7 @@ import collections
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -29,7 +30,7 @@ def short(name):
 
 def family(name):
     n = short(name)
-    if n.startswith("ssm_scan_kernel<64, 0"):
+    if re.search(r"(^|::)ssm_scan_kernel<64, [02],", n):  # tree modes, either lane layout
         return "ssm_scan"
     if n.startswith("gemm_f32_kernel"):
         return "gemm_f32"

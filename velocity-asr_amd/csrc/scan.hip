@@ -173,6 +173,22 @@ __device__ __forceinline__ void flush_half(float (&yv)[T], float* yp, int dl, in
     for (int j = 0; j < HalfReduce<G>::SF; ++j) yp[dl * TP + HALF * 8 + HalfReduce<G>::step(j, g)] = v[j];
 }
 
+// a * b + c: two roundings as in the reference tree (modes 0), or one fused multiply-add
+// (mode 2: v_pk_fma_f32, a third fewer state-update instructions)
+template <bool FMA>
+__device__ __forceinline__ f2 mad2(f2 a, f2 b, f2 c) {
+#pragma clang fp contract(off)
+    if constexpr (FMA) {
+#if VASR_SCAN_PACKED
+        return __builtin_elementwise_fma(a, b, c);
+#else
+        return f2{__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)};
+#endif
+    } else {
+        return a * b + c;
+    }
+}
+
 __device__ __forceinline__ f2 exp2v(f2 v) {
     f2 r;
     r.x = __builtin_amdgcn_exp2f(v.x);
@@ -199,7 +215,8 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
                                int L, int Di, int N, int mode, void* stream) {
     using namespace vasr;
     VASR_CHECK_ARG(xz && dt && bc && A2 && D && out, "vasr_ssm_scan_f32: null pointer");
-    VASR_CHECK_ARG(mode == 0 || mode == 1, "vasr_ssm_scan_f32: mode must be 0 (tree) or 1 (recurrence)");
+    VASR_CHECK_ARG(mode >= 0 && mode <= 2,
+                   "vasr_ssm_scan_f32: mode must be 0 (tree), 1 (recurrence) or 2 (tree, fused multiply-adds)");
     VASR_CHECK_ARG(B >= 0 && L >= 0 && L <= 8192 && Di > 0, "vasr_ssm_scan_f32: bad shape B=%d L=%d Di=%d", B, L, Di);
     VASR_CHECK_ARG(ld_xz % 4 == 0 && ld_dt % 4 == 0 && ld_bc % 4 == 0 && Di % 4 == 0,
                    "vasr_ssm_scan_f32: leading dims and Di must be multiples of 4");
@@ -220,8 +237,9 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
     const long waves4 = (long)B * Di * N / 256;
     const bool two = npl_env == 2 || (npl_env != 4 && waves4 < 512);
 #define VASR_SCAN_N(NS, NN)                                                                                   \
-    (mode == 0 ? NS::launch_n<NN, 0>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)         \
-               : NS::launch_n<NN, 1>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s))
+    (mode == 0   ? NS::launch_n<NN, 0>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)       \
+     : mode == 2 ? NS::launch_n<NN, 2>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)       \
+                 : NS::launch_n<NN, 1>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s))
     switch (N) {
         case 16: return two ? VASR_SCAN_N(npl2, 16) : VASR_SCAN_N(npl4, 16);
         case 32: return two ? VASR_SCAN_N(npl2, 32) : VASR_SCAN_N(npl4, 32);
