@@ -11,41 +11,49 @@ namespace {
 
 constexpr int kMaxPerLane = 16;  // C <= 1024
 
+// CPL: floats per lane as a compile-time constant when C = 64 * CPL (the model's C = 192 is
+// CPL = 3), so every load and store is unguarded and all of a row's loads issue before the
+// first reduction; CPL = 0 is the generic path (C <= 1024, per-element guards).  Both add the
+// same values in the same order (the generic path's extra terms are exact zeros), so the
+// result is bitwise the same.
+template <int CPL>
 __device__ __forceinline__ void ln_row_to(const float* __restrict__ x, const float* __restrict__ w,
                                           const float* __restrict__ b, float* __restrict__ y, int C,
                                           float eps, int lane) {
-    float v[kMaxPerLane];
+    constexpr int PL = CPL > 0 ? CPL : kMaxPerLane;
+    float v[PL];
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxPerLane; ++i) {
+    for (int i = 0; i < PL; ++i) {
         const int c = i * 64 + lane;
-        v[i] = (c < C) ? x[c] : 0.f;
+        v[i] = (CPL > 0 || c < C) ? x[c] : 0.f;
         s += v[i];
     }
     const float mean = wave_sum(s) / (float)C;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < kMaxPerLane; ++i) {
+    for (int i = 0; i < PL; ++i) {
         const int c = i * 64 + lane;
-        const float d = (c < C) ? v[i] - mean : 0.f;
+        const float d = (CPL > 0 || c < C) ? v[i] - mean : 0.f;
         q += d * d;
     }
     const float var = wave_sum(q) / (float)C;
     const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
-    for (int i = 0; i < kMaxPerLane; ++i) {
+    for (int i = 0; i < PL; ++i) {
         const int c = i * 64 + lane;
-        if (c < C) y[c] = __builtin_fmaf((v[i] - mean) * rstd, w[c], b[c]);  // as the GEMM LN prologue
+        if (CPL > 0 || c < C) y[c] = __builtin_fmaf((v[i] - mean) * rstd, w[c], b[c]);  // as the GEMM LN prologue
     }
 }
 
+template <int CPL>
 __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict__ x, int64_t ldx,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ b, float* y,
                                                          int64_t ldy, int rows, int C, float eps) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
-    ln_row_to(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
+    ln_row_to<CPL>(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
 }
 
 #ifndef VASR_DW_TT
@@ -62,7 +70,11 @@ constexpr int kMaxK = 8;
 // the history rows unroll without runtime guards; KC = 0 is the generic path (Kc <= kMaxK at
 // run time).  A runtime Kc turned every tap load and window read into its own guarded basic
 // block with a wait, serialising ~8 global-load latencies per thread (13.5 -> 4 us at B = 16).
-template <int KC>
+// CPT: floats per lane of a row as a compile-time constant (C = 64 * CPT; the model's 192 is 3),
+// 0 = generic (C <= kMaxC, guarded columns).  The channel's taps and bias are loaded before
+// phase 1 (C <= kMaxC = 256 threads: one channel per thread), so their latency overlaps the
+// row loads instead of following the barrier.
+template <int KC, int CPT>
 __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b,
@@ -80,7 +92,22 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     // Each wave normalises rows wave, wave + 4, ...: all of its row loads are issued before
     // the first reduction, so the rows' load latencies and butterfly chains overlap.
     constexpr int RPW = (TT + KM - 1 + 3) / 4;
-    constexpr int CPL = kMaxC / 64;
+    constexpr int CPL = CPT > 0 ? CPT : kMaxC / 64;
+    const int c_own = threadIdx.x;  // phase-2 channel (C <= 256)
+    float w[KM];
+    float bias = 0.f;
+    if (c_own < C) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) w[j] = (KC > 0 || j < Kc) ? cw[c_own * Kc + j] : 0.f;
+        bias = cb[c_own];
+    }
+    float lw[CPL], lb[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        const int col = c * 64 + lane;
+        lw[c] = (CPT > 0 || col < C) ? ln_w[col] : 0.f;
+        lb[c] = (CPT > 0 || col < C) ? ln_b[col] : 0.f;
+    }
     float v[RPW][CPL];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
@@ -90,7 +117,7 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int col = c * 64 + lane;
-            v[i][c] = (ok && col < C) ? xb[(int64_t)t * C + col] : 0.f;
+            v[i][c] = (ok && (CPT > 0 || col < C)) ? xb[(int64_t)t * C + col] : 0.f;
         }
     }
     float mean[RPW], rstd[RPW];
@@ -106,7 +133,7 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
         float q = 0.f;
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const float d = (c * 64 + lane < C) ? v[i][c] - mean[i] : 0.f;
+            const float d = (CPT > 0 || c * 64 + lane < C) ? v[i][c] - mean[i] : 0.f;
             q += d * d;
         }
         rstd[i] = 1.0f / sqrtf(wave_sum(q) / (float)C + eps);
@@ -120,20 +147,17 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int col = c * 64 + lane;
-            if (col < C) dst[col] = t < 0 ? 0.f : (v[i][c] - mean[i]) * rstd[i] * ln_w[col] + ln_b[col];
+            if (CPT > 0 || col < C) dst[col] = t < 0 ? 0.f : (v[i][c] - mean[i]) * rstd[i] * lw[c] + lb[c];
         }
     }
     __syncthreads();
     float* yb = y + (int64_t)b * L * C;
     const int rows = min(TT, L - t0);
-    for (int c = threadIdx.x; c < C; c += 256) {
-        float w[KM], win[KM];
+    if (c_own < C) {
+        const int c = c_own;
+        float win[KM];
 #pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            w[j] = (KC > 0 || j < Kc) ? cw[c * Kc + j] : 0.f;
-            win[j] = (j < Kc - 1) ? tile[j * C + c] : 0.f;
-        }
-        const float bias = cb[c];
+        for (int j = 0; j < KM; ++j) win[j] = (j < Kc - 1) ? tile[j * C + c] : 0.f;
         if (KC > 0 && rows == TT) {
             // full tile: every LN row read up front, outputs in straight-line code
             float lv[TT];
@@ -149,7 +173,7 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
                 }
                 yb[(int64_t)(t0 + tt) * C + c] = acc + bias;
             }
-            continue;
+            return;
         }
         for (int tt = 0; tt < rows; ++tt) {
             // window = LN rows tt .. tt + Kc - 1 of the tile (inputs t - Kc + 1 .. t)
@@ -196,8 +220,13 @@ VASR_API int vasr_layer_norm_f32(const float* x, int64_t ldx, const float* w, co
     VASR_CHECK_ARG(x && w && b && y, "vasr_layer_norm_f32: null pointer");
     VASR_CHECK_ARG(C > 0 && C <= 64 * kMaxPerLane && rows >= 0, "vasr_layer_norm_f32: bad shape rows=%d C=%d", rows, C);
     if (rows == 0) return VASR_OK;
-    hipLaunchKernelGGL(layer_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, ldx, w, b, y,
-                       ldy, rows, C, eps);
+    const dim3 grid((rows + 3) / 4), block(256);
+    hipStream_t s = as_stream(stream);
+    switch (C) {
+        case 192: hipLaunchKernelGGL(layer_norm_kernel<3>, grid, block, 0, s, x, ldx, w, b, y, ldy, rows, C, eps); break;
+        case 384: hipLaunchKernelGGL(layer_norm_kernel<6>, grid, block, 0, s, x, ldx, w, b, y, ldy, rows, C, eps); break;
+        default: hipLaunchKernelGGL(layer_norm_kernel<0>, grid, block, 0, s, x, ldx, w, b, y, ldy, rows, C, eps); break;
+    }
     return launch_status("vasr_layer_norm_f32");
 }
 
@@ -210,11 +239,13 @@ VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* 
     VASR_CHECK_ARG(C > 0 && C <= kMaxC && Kc >= 1 && Kc <= kMaxK && B >= 0 && L >= 0,
                    "vasr_ln_dwconv_f32: unsupported shape C=%d Kc=%d", C, Kc);
     if (B == 0 || L == 0) return VASR_OK;
-    if (Kc == 4)
-        hipLaunchKernelGGL(ln_dwconv_kernel<4>, dim3((L + TT - 1) / TT, B), dim3(256), 0, as_stream(stream), x, ln_w,
-                           ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+    const dim3 grid((L + TT - 1) / TT, B), block(256);
+    hipStream_t s = as_stream(stream);
+    if (Kc == 4 && C == 192)
+        hipLaunchKernelGGL((ln_dwconv_kernel<4, 3>), grid, block, 0, s, x, ln_w, ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+    else if (Kc == 4)
+        hipLaunchKernelGGL((ln_dwconv_kernel<4, 0>), grid, block, 0, s, x, ln_w, ln_b, conv_w, conv_b, y, L, C, Kc, eps);
     else
-        hipLaunchKernelGGL(ln_dwconv_kernel<0>, dim3((L + TT - 1) / TT, B), dim3(256), 0, as_stream(stream), x, ln_w,
-                           ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+        hipLaunchKernelGGL((ln_dwconv_kernel<0, 0>), grid, block, 0, s, x, ln_w, ln_b, conv_w, conv_b, y, L, C, Kc, eps);
     return launch_status("vasr_ln_dwconv_f32");
 }
