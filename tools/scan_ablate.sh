@@ -3,13 +3,14 @@
 # them with tools/scan_ablate_run.py.  VARIANTS="name:flags ..." (defaults below).
 set -e
 cd "$(dirname "$0")/../velocity-asr_amd"
-rm -rf ../tools/_ablate && mkdir -p ../tools/_ablate
+OUT=../tools/${VARIANT_DIR:-_variants}
+rm -rf $OUT && mkdir -p $OUT
 VARIANTS=${VARIANTS:-"w3:-DVASR_SCAN_WAVES=3 w2:-DVASR_SCAN_WAVES=2 w4:-DVASR_SCAN_WAVES=4 noexp:-DVASR_SCAN_ABLATE=1"}
 i=0
 for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include ${flags//,/ } \
-     -shared csrc/scan.hip csrc/common.cpp -o ../tools/_ablate/libscan_${i}_${name}.so &
+     -fno-slp-vectorize -ffp-contract=off -shared csrc/scan.hip csrc/common.cpp -o $OUT/lib_${i}_${name}.so &
   i=$((i+1))
 done
 wait

@@ -11,7 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def main():
-    B, L, Di, N = 32, 501, 384, 64
+    B, L, Di, N = int(os.environ.get("SCAN_B", 32)), 501, 384, 64
+    modes = tuple(int(m) for m in os.environ.get("SCAN_MODES", "0").split(","))
     M = B * L
     g = torch.Generator(device="cuda").manual_seed(0)
     xz = torch.randn(M, 2 * Di, device="cuda", generator=g)
@@ -31,10 +32,10 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     args = lambda mode: (xz.data_ptr(), 2 * Di, dt.data_ptr(), Di, bc.data_ptr(), 2 * N, A2.data_ptr(), D.data_ptr(),
                          out.data_ptr(), Di, B, L, Di, N, mode, st)
-    res = {n: [] for n, _ in fns}
+    res = {}
     for rnd in range(5):
         for n, f in fns:
-            for mode in (0,):
+            for mode in modes:
                 f(*args(mode))
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,7 +44,7 @@ def main():
                     assert f(*args(mode)) == 0
                 e.record()
                 torch.cuda.synchronize()
-                res[n].append(s.elapsed_time(e) / 20 * 1e3)
+                res[f"{n} m{mode}"] = res.get(f"{n} m{mode}", []) + [s.elapsed_time(e) / 20 * 1e3]
     for n, v in res.items():
         print(f"{n:20s} median {sorted(v)[len(v)//2]:8.1f} us  min {min(v):8.1f}")
 

@@ -47,6 +47,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef VASR_SCAN_WAVES_NPL2
 #define VASR_SCAN_WAVES_NPL2 4  // the same for the 2-states-per-lane layout
 #endif
+#ifndef VASR_SCAN_FASTSTAGE
+#define VASR_SCAN_FASTSTAGE 1  // 0: every chunk's staging addresses from the clamped index path
+#endif
 #ifndef VASR_SCAN_PACKED
 #define VASR_SCAN_PACKED 1  // 1: state pairs as float2 vectors (v_pk_*_f32); 0: scalar pairs
 #endif
@@ -64,6 +67,7 @@ __device__ __forceinline__ f2 operator*(f2 a, f2 b) { return f2{a.x * b.x, a.y *
 __device__ __forceinline__ f2 operator+(f2 a, f2 b) { return f2{a.x + b.x, a.y + b.y}; }
 #endif
 
+constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr int T = 16;    // time steps per chunk
 constexpr int TP = T + 1;  // padded row of the per-channel partial-sum tile
 constexpr int NW = 4;    // waves per block
