@@ -28,6 +28,7 @@
 // Operand maps (cdna_hip_programming.md §3): lane (r = lane & 31, h = lane >> 5) supplies
 // A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7.  The accumulator layout equals the
 // f32-input MFMA's, so gemm_common.h's epilogues apply.
+#include <cstdlib>
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -446,12 +447,22 @@ constexpr TileCfg kCfgs[] = {
     {2, 2, 1, 1, 4},  //  64 x  64
 };
 
+// Tiles a launch needs for the larger tile shapes (default 1.9 per CU).  VASR_X3_MIN_TILES
+// overrides it (read once; diagnostic: launches that run beside another stream's work).
+static long x3_min_tiles() {
+    static const long v = [] {
+        const char* e = std::getenv("VASR_X3_MIN_TILES");
+        return e ? std::atol(e) : 19L * kCUs / 10;
+    }();
+    return v;
+}
+
 int pick_x3(int M, int N, int batch, bool pair, bool ln = false) {
     for (int i = ln ? 1 : 0; i < 2; ++i) {
         const TileCfg& c = kCfgs[i];
         const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
         const bool exact_n = N % c.bn() == 0 || N > 4 * c.bn();  // little padding waste
-        if (tiles >= 19 * kCUs / 10 && exact_n) return i;
+        if (tiles >= x3_min_tiles() && exact_n) return i;
     }
     return pair ? 1 : 2;  // paired epilogues need an even TN
 }
