@@ -184,3 +184,16 @@ def test_mamba_mode_and_bad_mode():
     v.SelectiveSSM(scan_mode="mamba")  # served by the HIP recurrence kernel
     with pytest.raises(ValueError):
         v.SelectiveSSM(scan_mode="bogus")
+
+
+def test_tree_scan_kernel_mode_selection(monkeypatch):
+    """scan_mode="parallel" runs kernel mode 2 (fused multiply-adds) unless VASR_SCAN_FMA=0
+    selects mode 0 (the reference tree op for op); the other modes map to the recurrence."""
+    from velocity_asr import ssm
+    monkeypatch.delenv("VASR_SCAN_FMA", raising=False)
+    assert ssm._tree_mode() == 2
+    monkeypatch.setenv("VASR_SCAN_FMA", "0")
+    assert ssm._tree_mode() == 0
+    monkeypatch.setenv("VASR_SCAN_FMA", "1")
+    assert ssm._tree_mode() == 2
+    assert ssm._SCAN_MODE_ID == {"parallel": 0, "sequential": 1, "mamba": 1}
