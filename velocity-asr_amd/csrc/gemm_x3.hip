@@ -447,14 +447,17 @@ constexpr TileCfg kCfgs[] = {
     {2, 2, 1, 1, 4},  //  64 x  64
 };
 
-// Tiles a launch needs for the larger tile shapes (default 1.9 per CU).  VASR_X3_MIN_TILES
-// overrides it (read once; diagnostic: launches that run beside another stream's work).
-static long x3_min_tiles() {
+// Tiles a launch needs before a larger tile shape is taken: 1.9 per CU for 128 x 128, 1.4 per
+// CU for 128 x 64 (FFN1 at the bench's 16-clip M = 8016: 378 tiles of 128 x 64 measured 1-1.5 %
+// faster end to end than 756 of 64 x 64; N = 192 at 189 tiles stays on 64 x 64, 4 % faster).
+// VASR_X3_MIN_TILES overrides both (read once; diagnostic).
+static long x3_min_tiles(int cfg) {
     static const long v = [] {
         const char* e = std::getenv("VASR_X3_MIN_TILES");
-        return e ? std::atol(e) : 19L * kCUs / 10;
+        return e ? std::atol(e) : 0L;
     }();
-    return v;
+    if (v > 0) return v;
+    return cfg == 0 ? 19L * kCUs / 10 : 14L * kCUs / 10;
 }
 
 int pick_x3(int M, int N, int batch, bool pair, bool ln = false) {
@@ -462,7 +465,7 @@ int pick_x3(int M, int N, int batch, bool pair, bool ln = false) {
         const TileCfg& c = kCfgs[i];
         const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
         const bool exact_n = N % c.bn() == 0 || N > 4 * c.bn();  // little padding waste
-        if (tiles >= x3_min_tiles() && exact_n) return i;
+        if (tiles >= x3_min_tiles(i) && exact_n) return i;
     }
     return pair ? 1 : 2;  // paired epilogues need an even TN
 }
