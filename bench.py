@@ -4,22 +4,33 @@
 Workload (BASELINE.json configs[1]): the 6.17 M-parameter fp32 model, batch of 32 synthetic
 10 s clips at 16 kHz per GPU.  One step = real-FFT |STFT|^2 + log-mel + full forward
 (temporal binding, 8 SSM blocks, hierarchical global context, CTC head) + argmax + greedy
-collapse, on audio already resident in HBM, replayed as one HIP graph.  Multi-GPU: one
-process per GPU (torchrun), each rank transcribes its own 32 clips (utterance sharding, no
-data-path collective; weak scaling); a barrier + synchronize brackets the K timed steps
-and the max time over ranks is used.
+collapse, on audio already resident in HBM, replayed as HIP graphs.
+
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` without WORLD_SIZE starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child process (before
+anything touches the GPU) and exits with its code; under torchrun every rank joins an RCCL
+("nccl") process group, world size 1 included.  Each rank transcribes its own 32 clips
+(utterance sharding, no data-path collective; weak scaling); a barrier + synchronize brackets
+the K timed steps and the max time over ranks is used.  A second timed leg ("with_scatter")
+runs the serving form: rank 0 holds the whole (N*32, S) batch in HBM, each step scatters the
+shards over RCCL (xGMI) straight into every rank's graph input, replays, and gathers the int32
+tokens back to rank 0 (velocity_asr.distributed.transcribe_sharded).
 
 Prints ONE JSON line (rank 0):
-  value         = RTFx = audio seconds transcribed by all ranks / wall seconds
-  roofline      = the dominant kernel family measured live with HIP events (eager replay of
-                  the same steps on the launch stream) against the MI355X peak
-  cpu_baseline  = the numpy restatement of the reference path (oracle/) on this host, a
-                  bounded sample of the same workload (rank 0, N=1 only)
+  value         = RTFx = audio seconds transcribed by all ranks / wall seconds (resident inputs)
+  roofline      = the dominant kernel measured live with HIP events (eager replay of the same
+                  steps on the launch stream) against the MI355X peak; flat scalar fields add
+                  the scan's VALU roof, the HBM ceiling its arithmetic allows, and the GEMM
+                  family's MFMA fraction
+  cpu_baseline  = the numpy restatement of the reference path (oracle/) with the reference's
+                  materialised tree scan, timed on this host (rank 0, N=1 only)
 """
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,12 +47,77 @@ METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 SR = 16000
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA (no sparsity)
+F32_MFMA_PEAK_TFS = 157.3    # f32-input MFMA = fp32 vector peak
 F32_VALU_PEAK_TOPS = 78.6    # fp32 vector lane-operations/s (157.3 TFLOP/s with FMA = 2 flops)
 VALU_OPS_PER_ELEM = 11       # reference tree scan, fp32 ops per state element (SURVEY §8 d)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--seconds", type=float, default=10.0, help="clip length")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-scatter", action="store_true", help="skip the scatter/gather serving leg")
+    ap.add_argument("--inproc", action="store_true",
+                    help="run a single rank in this process instead of through torch.distributed.run")
+    ap.add_argument("--roofline-steps", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=0,
+                    help="utterance groups replayed as separate HIP graphs on concurrent streams (the scan of one "
+                         "group overlaps the GEMMs of the other; results are bitwise those of one graph); "
+                         "0 = 2 when the batch is >= 8 clips, else 1")
+    ap.add_argument("--int8", action="store_true",
+                    help="BASELINE configs[4]: INT8 fake-quant model (prepare_model_for_qat + activation calibration)")
+    ap.add_argument("--bf16", action="store_true",
+                    help="BASELINE configs[2] per-GPU shape: the model as bf16 (bf16 weights / MFMA operands)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args) -> int:
+    """Start N ranks with torch.distributed.run as a child process (this process never touches
+    the GPU: torch.cuda.device_count() does not initialise HIP on this image)."""
+    visible = torch.cuda.device_count()
+    if visible < args.gpus:
+        log(f"bench.py: --gpus {args.gpus} requested but only {visible} GPU(s) are visible")
+        return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class stdout_to_stderr:
+    """Point file descriptor 1 at stderr for the duration (library banners written by native
+    code would otherwise precede the one JSON line on stdout)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
 
 
 def build_model(device):
@@ -81,7 +157,7 @@ def kernel_roofline(model, audio, steps, streams=1):
         elems = i["B"] * i["L"] * i["Di"] * i["N"]
         t = float(np.mean([d for d, _ in scans]))
         out["scan"] = dict(t=t, bytes=bytes_per, elems=elems, launches=len(scans), per_step=len(scans) / steps,
-                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"])
+                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"], N=i["N"])
     g = rec["gemm"]
     flops = [2.0 * i["M"] * i["N"] * i["K"] * i["batch"] for _, i in g]
     groups = {}
@@ -92,13 +168,27 @@ def kernel_roofline(model, audio, steps, streams=1):
     out["gemm"] = dict(t=float(np.mean([d for d, _ in g])), flops=float(np.mean(flops)), launches=len(g),
                        per_step=len(g) / steps, total=sum(d for d, _ in g) / steps,
                        tflops=sum(flops) / max(sum(d for d, _ in g), 1e-12) / 1e12,
-                       top_shape="M=%d N=%d K=%d batch=%d" % top[0], top_t=float(np.mean([d for d, _ in top[1]])),
+                       top_shape="M=%d N=%d K=%d batch=%d" % top[0], top_key=top[0],
+                       top_t=float(np.mean([d for d, _ in top[1]])),
                        top_flops=top[1][0][1], top_total=sum(d for d, _ in top[1]) / steps)
     return out
 
 
-def cpu_baseline(seconds_target=12.0):
-    """Oracle (numpy port of the reference path) on 10 s clips until ~seconds_target of work."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds_target=15.0, chunk=4):
+    """The oracle (numpy restatement of the reference path) with the reference's materialised
+    tree scan (ssm.py:216-295: (B, P, Di, N) up/down-sweep), on the bench's own clips
+    (make_audio(32, 160000, seed=1234)) in batches of `chunk`, until ~seconds_target of work."""
     from oracle import velocity_ref as R
     from velocity_asr import synthetic as S
     try:
@@ -108,45 +198,75 @@ def cpu_baseline(seconds_target=12.0):
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     W = S.make_weights(None, seed=0)
     cfg = dict(S.DEFAULT_CONFIG)
+    audio = S.make_audio(32, 10 * SR, seed=1234)
+    prev, R.SCAN_FORM = R.SCAN_FORM, "tree"
     clips, t0 = 0, time.perf_counter()
-    while True:
-        a = S.make_audio(1, 10 * SR, seed=1234 + clips)
-        R.ctc_greedy_decode(R.forward(W, R.compute_mel_spectrogram(a), cfg))
-        clips += 1
-        el = time.perf_counter() - t0
-        if el >= seconds_target or clips >= 32:
-            break
+    try:
+        while clips < audio.shape[0]:
+            a = audio[clips:clips + chunk]
+            R.ctc_greedy_decode(R.forward(W, R.compute_mel_spectrogram(a), cfg))
+            clips += a.shape[0]
+            if time.perf_counter() - t0 >= seconds_target:
+                break
+    finally:
+        R.SCAN_FORM = prev
+    el = time.perf_counter() - t0
     return dict(value=round(clips * 10.0 / el, 3), unit="audio-sec/sec (RTFx)", cores=int(threads), kind="port",
-                sample=f"{clips} x 10 s clips, batch 1, mel+forward+greedy, oracle/velocity_ref.py "
-                       f"(numpy, BLAS threads={threads}), {el:.1f} s wall")
+                sample=f"first {clips} of the bench's 32 x 10 s clips in batches of {chunk}, mel+forward+greedy, "
+                       f"oracle/velocity_ref.py with the reference's materialised tree scan (SCAN_FORM='tree'), "
+                       f"numpy BLAS threads={threads}, {el:.1f} s wall; host CPU: {cpu_model()}, "
+                       f"os.cpu_count()={os.cpu_count()}; the real reference measured 7.95 RTFx on 8 Xeon "
+                       f"threads in the build container (SURVEY §6)")
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
-    ap.add_argument("--seconds", type=float, default=10.0, help="clip length")
-    ap.add_argument("--eager", action="store_true", help="time eager launches instead of the HIP graph")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--roofline-steps", type=int, default=3)
-    ap.add_argument("--streams", type=int, default=2,
-                    help="utterance groups replayed as separate HIP graphs on concurrent streams (the scan of one "
-                         "group overlaps the GEMMs of the other; results are bitwise those of one graph)")
-    ap.add_argument("--int8", action="store_true",
-                    help="BASELINE configs[4]: INT8 fake-quant model (prepare_model_for_qat + activation calibration)")
-    ap.add_argument("--bf16", action="store_true",
-                    help="BASELINE configs[2] per-GPU shape: the model as bf16 (bf16 weights / MFMA operands)")
-    args = ap.parse_args()
+def golden_check(toks, lens, args):
+    """Rank 0's tokens vs the reference's greedy lists for the same clips (tests/golden/
+    fwd_fullbatch.npz: make_audio(32, 160000, seed=1234)), when the workload is that batch."""
+    path = os.path.join(REPO, "tests", "golden", "fwd_fullbatch.npz")
+    if args.bf16 or args.int8 or args.batch != 32 or args.seconds != 10.0 or not os.path.exists(path):
+        return None
+    from velocity_asr.pipeline import token_lists
+    g = np.load(path, allow_pickle=False)
+    return token_lists(toks, lens) == json.loads(str(g["greedy"]))["c2"]
 
+
+def pmc_lookup(name, key=None):
+    path = os.path.join(REPO, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d if key is None else d.get(key)
+    except Exception:
+        return None
+
+
+def timed(step, steps, world, dev):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def run(args):
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    distributed = "WORLD_SIZE" in os.environ
 
     from velocity_asr import synthetic as S
     from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids
@@ -162,53 +282,78 @@ def main():
         Q.calibrate_from_activations(model, compute_mel_spectrogram(calib))
     S_len = int(args.seconds * SR)
     B = args.batch
+    streams = args.streams or (2 if B >= 8 else 1)
     audio = torch.from_numpy(S.make_audio(B, S_len, seed=1234 + rank)).to(dev)  # resident in HBM
 
     if args.eager:
         def step():
             return audio_to_token_ids(model, audio)
+        tr = None
     else:
-        tr = GraphedTranscriber(model, B, S_len, dev, streams=args.streams)
+        tr = GraphedTranscriber(model, B, S_len, dev, streams=streams)
         tr.audio.copy_(audio)
         step = tr.step
 
+    # RCCL joins after the graph streams exist: HIP deals streams round-robin onto the
+    # process's few hardware queues (GPU_MAX_HW_QUEUES = 4), and a communicator created first
+    # takes queues in that rotation so that the two utterance-group streams can land on one
+    # queue and serialise (measured 4.0 vs 2.7 ms per step)
+    if distributed:
+        with stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator creation
+            dist.init_process_group("nccl", device_id=dev)
+            dist.barrier()
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(step, args.steps, world, dev)
 
-    # token checksum over all ranks (tiny gather, outside the timed region); the timed graph's
-    # own output must equal an eager pass over the same audio
+    # tokens of the timed graph vs an eager pass over the same audio, and vs the reference's
+    # greedy lists for the same clips (outside the timed region)
     toks, lens = audio_to_token_ids(model, audio)
     graph_match = True
-    if not args.eager:
+    if tr is not None:
         from velocity_asr.pipeline import token_lists
         gt, gl = tr.collect()
         graph_match = token_lists(gt, gl) == token_lists(toks, lens)
+    golden_ok = golden_check(toks, lens, args) if rank == 0 else None
     valid = torch.arange(toks.shape[1], device=dev)[None, :] < lens[:, None]
     csum = torch.tensor([float(lens.sum().item()), float(toks.long().masked_fill(~valid, 0).sum().item())],
                         device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(csum)
 
-    rf = kernel_roofline(model, audio, args.roofline_steps, 1 if args.eager else args.streams)
+    # serving leg: scatter from rank 0 over RCCL into each rank's graph input, gather tokens
+    scatter = None
+    if distributed and tr is not None and not args.no_scatter:
+        from velocity_asr.distributed import graphed_step, transcribe_sharded
+        full = None
+        if rank == 0:
+            full = torch.cat([torch.from_numpy(S.make_audio(B, S_len, seed=1234 + r)) for r in range(world)]).to(dev)
+        gstep = graphed_step(tr)
+        res = {}
+
+        def sstep():
+            res["out"] = transcribe_sharded(gstep, full, world * B, S_len, dev, shard=tr.audio, as_lists=False)
+        for _ in range(max(2, args.warmup // 2)):
+            sstep()
+        el_s = timed(sstep, args.steps, world, dev)
+        ok = None
+        if rank == 0:
+            # the gathered block for rank 0's shard equals the resident-path tokens
+            ta, la = res["out"]
+            from velocity_asr.pipeline import token_lists
+            ok = token_lists(ta[:B], la[:B]) == token_lists(toks, lens)
+        scatter = dict(value=round(world * B * args.seconds * args.steps / el_s, 2),
+                       ms_per_step=round(el_s / args.steps * 1e3, 3),
+                       scatter_mb_per_rank=round(B * S_len * 4 / 1e6, 2),
+                       gather_kb_per_rank=round(B * (toks.shape[1] + 1) * 4 / 1e3, 1),
+                       rank0_tokens_match=ok)
+        tr.audio.copy_(audio)
+
+    rf = kernel_roofline(model, audio, args.roofline_steps, 1 if args.eager else streams)
     if world > 1:
         dist.barrier()
     if rank != 0:
-        if world > 1:
+        if distributed:
             dist.destroy_process_group()
         return
 
@@ -216,34 +361,49 @@ def main():
     frames = world * B * (S_len // 160 + 1) * args.steps
     ms_per_step = elapsed / args.steps * 1e3
     sc, gm = rf.get("scan"), rf["gemm"]
+    # GEMM family: split-bf16 ("x3") products = six bf16 MFMA products per fp32 multiply-add
+    x3 = not args.bf16 and os.environ.get("VASR_GEMM", "x3") == "x3"
+    prod = 6 if x3 else 1
+    g_ach = prod * gm["top_flops"] / gm["top_t"] / 1e12
+    g_f32 = gm["top_flops"] / gm["top_t"] / 1e12
+    gemm_fields = dict(gemm_kernel=f"vasr gemm {'x3 (6 bf16 products)' if x3 else 'bf16' if args.bf16 else 'f32'} "
+                                   f"{gm['top_shape']}",
+                       gemm_avg_launch_us=round(gm["top_t"] * 1e6, 2),
+                       gemm_achieved=round(g_ach, 2), gemm_peak=BF16_MFMA_PEAK_TFS, gemm_unit="TFLOP/s",
+                       gemm_frac=round(g_ach / BF16_MFMA_PEAK_TFS, 4),
+                       gemm_f32eq_tflops=round(g_f32, 2), gemm_f32eq_frac=round(g_f32 / F32_MFMA_PEAK_TFS, 4),
+                       gemm_all_f32eq_tflops=round(gm["tflops"], 2))
+    mf = pmc_lookup("pmc_mfma.json")
+    if isinstance(mf, dict):
+        ent = mf.get("%d,%d,%d" % gm["top_key"][:3])
+        if isinstance(ent, dict):
+            gemm_fields["gemm_mfma_busy_frac"] = ent.get("mfma_busy_frac")
     # dominant kernel = the single kernel (same code, same shape) with the largest time per step
     if sc and sc["total"] >= gm["top_total"]:
         ach = sc["bytes"] / sc["t"] / 1e9
         roof = dict(bound="hbm", kernel="vasr ssm_scan (tree scan + gate, 8 local blocks, B*L*(4*Di+2*N)*4 B/launch)",
                     achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                     traffic=None, avg_launch_us=round(sc["t"] * 1e6, 2))
-        # the scan is VALU-bound: the same launch against the fp32 vector roof, at the
-        # reference tree's ~11 fp32 operations per state element (SURVEY §8 d), FMA counted once
+        # the scan is VALU-bound: the same launch against the fp32 vector roof at the
+        # reference tree's ~11 fp32 operations per state element (SURVEY §8 d), and the HBM fraction
+        # that arithmetic allows at best: (bytes/elem / HBM peak) / (ops/elem / VALU peak)
         tops = sc["elems"] * VALU_OPS_PER_ELEM / sc["t"] / 1e12
-        roof["valu"] = dict(ops_per_element=VALU_OPS_PER_ELEM, achieved=round(tops, 2), peak=F32_VALU_PEAK_TOPS,
-                            unit="T lane-ops/s", frac=round(tops / F32_VALU_PEAK_TOPS, 4))
+        ceil = (sc["bytes"] / sc["elems"] / (HBM_PEAK_GBS * 1e9)) / (VALU_OPS_PER_ELEM / (F32_VALU_PEAK_TOPS * 1e12))
+        roof.update(valu_ops_per_element=VALU_OPS_PER_ELEM, valu_achieved=round(tops, 2),
+                    valu_peak=F32_VALU_PEAK_TOPS, valu_unit="T lane-ops/s", valu_frac=round(tops / F32_VALU_PEAK_TOPS, 4),
+                    hbm_ceiling_frac=round(ceil, 4), frac_of_hbm_ceiling=round(ach / HBM_PEAK_GBS / ceil, 4))
         key = "ssm_scan"
     else:
-        # split-bf16 GEMM: six bf16 MFMA products per fp32 multiply-add, against the dense bf16 roof
-        ach = 6 * gm["top_flops"] / gm["top_t"] / 1e12
-        roof = dict(bound="mfma", kernel=f"vasr gemm_x3 {gm['top_shape']} (6 bf16 products)", achieved=round(ach, 2),
-                    peak=BF16_MFMA_PEAK_TFS, unit="TFLOP/s", frac=round(ach / BF16_MFMA_PEAK_TFS, 4), traffic=None,
+        roof = dict(bound="mfma", kernel=gemm_fields["gemm_kernel"], achieved=round(g_ach, 2), peak=BF16_MFMA_PEAK_TFS,
+                    unit="TFLOP/s", frac=round(g_ach / BF16_MFMA_PEAK_TFS, 4), traffic=None,
                     avg_launch_us=round(gm["top_t"] * 1e6, 2))
         key = "gemm_x3"
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            t = json.load(open(pmc)).get(key)
-            if isinstance(t, dict) and sc:  # by launch grid: B x Di/16 blocks of 256 threads
-                t = t.get(str(sc["B"] * (sc["Di"] // 16) * 256))
-            roof["traffic"] = t
-        except Exception:
-            pass
+    roof.update(gemm_fields)
+    t = pmc_lookup("pmc_traffic.json", key)
+    if isinstance(t, dict) and sc and key == "ssm_scan":  # by launch grid: B x Di/16 blocks of 256 threads
+        t = t.get(str(sc["B"] * (sc["Di"] // 16) * 256))
+    if isinstance(t, (int, float)):
+        roof["traffic"] = t
     line = {
         "metric": METRIC,
         "value": round(audio_sec / elapsed, 2),
@@ -260,10 +420,13 @@ def main():
         "config": {"workload": f"{B} x {args.seconds:g} s clips per GPU, audio->mel->forward->CTC greedy tokens "
                                f"(BASELINE configs[{4 if args.int8 else 2 if args.bf16 else 1}]"
                                f"{', INT8 fake-quant' if args.int8 else ''}"
-                               f"{f', HIP graph x{args.streams} streams' if not args.eager else ', eager'})",
-                   "global_batch": world * B, "clip_seconds": args.seconds, "parallelism": f"utterance-shard x{world}"},
+                               f"{f', HIP graph x{streams} streams' if not args.eager else ', eager'})",
+                   "global_batch": world * B, "clip_seconds": args.seconds,
+                   "parallelism": f"utterance-shard x{world} over RCCL ({'resident shards; serving leg scatters from rank 0 and gathers tokens' if scatter else 'resident shards'})"
+                   if distributed else "single process"},
         "frames_per_sec": round(frames / elapsed, 1),
         "roofline": roof,
+        "with_scatter": scatter,
         "kernels": {
             "scan": None if not sc else dict(avg_launch_us=round(sc["t"] * 1e6, 2), launches_per_step=sc["per_step"],
                                              ms_per_step=round(sc["total"] * 1e3, 3),
@@ -274,12 +437,23 @@ def main():
         },
         "token_checksum": [int(csum[0].item()), int(csum[1].item())],
         "graph_tokens_match_eager": graph_match,
+        "rank0_tokens_match_reference": golden_ok,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and not args.inproc:
+        sys.exit(launch(args))
+    if args.inproc and args.gpus != 1:
+        log("bench.py: --inproc runs one rank; use --gpus 1")
+        sys.exit(2)
+    run(args)
 
 
 if __name__ == "__main__":

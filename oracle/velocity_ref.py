@@ -330,8 +330,16 @@ def associative_scan_stream(dA: np.ndarray, xdB: np.ndarray) -> np.ndarray:
     return out
 
 
-def parallel_scan(x, dt, A, Bm, Cm, D, stream: bool = True):
+# Form of the tree scan used by forward(): "stream" (O(log L) state, bitwise equal) or "tree"
+# (the reference's materialised (B, P, Di, N) up/down-sweep, its CPU cost profile; bench.py's
+# cpu_baseline times this form).
+SCAN_FORM = "stream"
+
+
+def parallel_scan(x, dt, A, Bm, Cm, D, stream: Optional[bool] = None):
     """_parallel_scan (ssm.py:173-214): y = einsum(h, C) + x*D with the tree scan."""
+    if stream is None:
+        stream = SCAN_FORM == "stream"
     dA, xdB = discretize(x, dt, A, Bm)
     h = associative_scan_stream(dA, xdB) if stream else associative_scan_tree(dA, xdB)
     y = np.einsum("bldn,bln->bld", h, Cm).astype(f32)

@@ -449,8 +449,70 @@ def gen_bf16():
     save("bf16_fwd.npz", **out)
 
 
+# --------------------------------------------------------------------------- full bench batches
+def _tokens_pack(prefix, model, audio, chunk, out, decoded):
+    """Reference forward over `audio` in chunks of `chunk` clips (the reference CPU path needs
+    ~0.5 GB per 10-s clip); argmax tokens, top-2 margin per frame, greedy lists."""
+    toks, margins, greedy = [], [], []
+    for i in range(0, audio.shape[0], chunk):
+        with torch.no_grad():
+            mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(audio[i:i + chunk]))
+            logits = model(mel)
+        top2 = torch.topk(logits, 2, dim=-1)
+        toks.append(logits.argmax(-1).numpy().astype(np.int16))
+        margins.append((top2.values[..., 0] - top2.values[..., 1]).numpy().astype(np.float32))
+        greedy.extend(ref_decode.ctc_greedy_decode(logits))
+        print(f"  {prefix}: clips {i}..{i + chunk - 1} done", flush=True)
+    out[prefix + "tokens"] = np.concatenate(toks)
+    out[prefix + "margin"] = np.concatenate(margins)
+    decoded[prefix.rstrip("_")] = greedy
+
+
+def gen_fullbatch():
+    """Every clip of the bench workloads pinned to the reference:
+    C2 = make_audio(32, 160000, seed=1234) (bench.py rank 0), all 32 clips, chunks of 8;
+    C4 = make_audio(32, 480000, seed=1234), the first 8 clips, chunks of 2."""
+    model = build_model()
+    out, decoded = {}, {}
+    _tokens_pack("c2_", model, syn.make_audio(32, 160000, seed=1234), 8, out, decoded)
+    _tokens_pack("c4_", model, syn.make_audio(32, 480000, seed=1234)[:8], 2, out, decoded)
+    out["greedy"] = np.array(json.dumps(decoded))
+    out["meta"] = meta(c2="make_audio(32, 160000, seed=1234), reference run in chunks of 8",
+                       c4="make_audio(32, 480000, seed=1234)[:8], reference run in chunks of 2",
+                       weights="make_weights(None, seed=0)")
+    save("fwd_fullbatch.npz", **out)
+
+
+# --------------------------------------------------------------------------- CLI output
+CLI_CLIPS = {"clip_2s.wav": ("make_audio(1, 32000, seed=91)[0]", lambda: syn.make_audio(1, 32000, seed=91)[0]),
+             "chirp_3s.wav": ("make_chirp(48000)", lambda: syn.make_chirp(48000)),
+             "clip_10s.wav": ("make_audio(2, 160000, seed=1234)[1]", lambda: syn.make_audio(2, 160000, seed=1234)[1])}
+
+
+def gen_cli():
+    """The reference's own scripts/transcribe.py:transcribe_file (text and --timestamps JSON).
+    Its load_audio needs torchaudio (absent), so the module's `load_audio` name is rebound to
+    return the clip; everything after it (mel, forward, decode, word grouping) is the reference."""
+    spec = importlib.util.spec_from_file_location("ref_transcribe_script", "/root/reference/scripts/transcribe.py")
+    tr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tr)
+    model = build_model()
+    decoder = ref_decode.CTCDecoder(ref_decode.create_default_vocabulary(1000))
+    res = {}
+    for name, (recipe, make) in CLI_CLIPS.items():
+        clip = torch.from_numpy(make())
+        tr.load_audio = lambda path, _c=clip: _c
+        res[name] = {"recipe": recipe,
+                     "text": tr.transcribe_file(model, name, decoder, "cpu", include_timestamps=False),
+                     "timestamps": tr.transcribe_file(model, name, decoder, "cpu", include_timestamps=True)}
+    with open(os.path.join(HERE, "cli_transcribe.json"), "w") as f:
+        json.dump({"meta": json.loads(str(meta(weights="make_weights(None, seed=0)"))), "clips": res}, f, indent=1)
+    print("wrote cli_transcribe.json")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8", "bf16", "beam"]
+    which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8", "bf16", "beam",
+                             "fullbatch", "cli"]
     if "mel" in which:
         gen_mel()
     if "scan" in which:
@@ -469,3 +531,7 @@ if __name__ == "__main__":
         gen_bf16()
     if "beam" in which:
         gen_beam()
+    if "fullbatch" in which:
+        gen_fullbatch()
+    if "cli" in which:
+        gen_cli()

@@ -53,8 +53,15 @@ def _worker(rank, world, port, audio, q):
     from velocity_asr.distributed import transcribe_sharded
     res = transcribe_sharded(fake_step, audio if rank == 0 else None, audio.shape[0], audio.shape[1],
                              torch.device("cpu"))
+    # device-tensor form (the bench's serving leg) into a caller-provided shard buffer
+    shard = torch.empty((audio.shape[0] // world, audio.shape[1]))
+    blocks = transcribe_sharded(fake_step, audio if rank == 0 else None, audio.shape[0], audio.shape[1],
+                                torch.device("cpu"), shard=shard, as_lists=False)
     if rank == 0:
-        q.put(res)
+        t, n = blocks
+        q.put((res, [t[i, : int(n[i])].tolist() for i in range(t.shape[0])]))
+    else:
+        assert blocks is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,13 +76,28 @@ def test_sharded_transcription_matches_single_process(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, audio, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=120)
+    res, res_blocks = q.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     toks, lens = fake_step(audio)
     expect = [toks[b, : lens[b]].tolist() for b in range(audio.shape[0])]
     assert res == expect
+    assert res_blocks == expect
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N with fewer visible GPUs exits non-zero with a clear message (the
+    launcher checks before starting torch.distributed.run)."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "--gpus 4 requested but only 0 GPU(s) are visible" in r.stderr
 
 
 def test_shard_range_partitions():

@@ -103,3 +103,25 @@ def test_graphed_streams_match_eager(va, streams):
     gt.step()
     torch.cuda.synchronize()
     assert token_lists(*gt.collect()) == token_lists(te, le)
+    # the static outputs are refreshed by every replay (all stream groups write their rows)
+    assert token_lists(gt.tokens, gt.lengths) == token_lists(te, le)
+    gt.audio.copy_(torch.flip(audio, [0]))
+    gt.step()
+    torch.cuda.synchronize()
+    assert token_lists(gt.tokens, gt.lengths) == token_lists(te, le)[::-1]
+
+
+def test_graphed_transcriber_refuses_changed_weights(va):
+    """Replaying graphs whose weights were modified (or whose derived layouts were rebuilt)
+    would read stale pointers: step() must raise instead."""
+    from velocity_asr.pipeline import GraphedTranscriber
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    gt = GraphedTranscriber(m, 2, 16000, streams=2)
+    gt.step()
+    with torch.no_grad():
+        m.ctc_head.proj[2].bias.add_(1.0)
+    with pytest.raises(RuntimeError, match="changed after capture"):
+        gt.step()

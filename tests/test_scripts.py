@@ -147,3 +147,26 @@ def test_evaluate_script_manifest_and_dir(ckpt_and_clips, tmp_path, capsys):
     assert ev.main(["--checkpoint", str(root / "model.pt"), "--audio-dir", str(clips), "--output", str(out2)]) == 0
     rows = dict(line.split("\t", 1) for line in out2.read_text().splitlines())
     assert rows == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("clip", ["clip_2s.wav", "chirp_3s.wav", "clip_10s.wav"])
+def test_transcribe_script_matches_reference_cli_output(ckpt_and_clips, tmp_path, capsys, clip):
+    """scripts/transcribe.py --format json [--timestamps] vs the reference's own
+    transcribe_file output for the same clip and weights (tests/golden/cli_transcribe.json,
+    captured from /root/reference/scripts/transcribe.py in the build container)."""
+    from velocity_asr.audio import write_wav
+    root, _ = ckpt_and_clips
+    g = golden_json("cli_transcribe.json")["clips"][clip]
+    recipe = g["recipe"]
+    make = {"make_audio(1, 32000, seed=91)[0]": lambda: S.make_audio(1, 32000, seed=91)[0],
+            "make_chirp(48000)": lambda: S.make_chirp(48000),
+            "make_audio(2, 160000, seed=1234)[1]": lambda: S.make_audio(2, 160000, seed=1234)[1]}[recipe]
+    path = tmp_path / clip
+    write_wav(str(path), make())
+    tr = _script("transcribe")
+    for key, extra in (("text", []), ("timestamps", ["--timestamps"])):
+        assert tr.main([str(path), "--checkpoint", str(root / "model.pt"), "--format", "json", "-q"] + extra) == 0
+        got = json.loads(capsys.readouterr().out)
+        exp = dict(g[key], file=str(path))
+        assert got == exp, key

@@ -10,9 +10,9 @@ OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python3 bench.py $ARGS > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
+    python3 bench.py --inproc $ARGS > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+    python3 bench.py --inproc --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 > "$OUT/bench_write.json" 2> "$OUT/write.err"
+    python3 bench.py --inproc --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 > "$OUT/bench_write.json" 2> "$OUT/write.err"
 echo done > "$OUT/DONE"

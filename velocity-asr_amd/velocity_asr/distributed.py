@@ -30,10 +30,14 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def scatter_audio(audio: Optional[torch.Tensor], per_rank: int, samples: int, device: torch.device,
-                  src: int = 0) -> torch.Tensor:
-    """Scatter (world*per_rank, samples) audio held by `src` into (per_rank, samples) shards."""
+                  src: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Scatter (world*per_rank, samples) audio held by `src` into (per_rank, samples) shards.
+    out: the destination shard (e.g. a GraphedTranscriber's static input), else allocated."""
     world = dist.get_world_size()
-    out = torch.empty((per_rank, samples), dtype=torch.float32, device=device)
+    if out is None:
+        out = torch.empty((per_rank, samples), dtype=torch.float32, device=device)
+    elif tuple(out.shape) != (per_rank, samples) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"scatter_audio: out must be a contiguous float32 ({per_rank}, {samples}) tensor")
     if dist.get_rank() == src:
         if audio is None or audio.shape != (world * per_rank, samples):
             raise ValueError(f"scatter_audio: src needs ({world * per_rank}, {samples}) audio")
@@ -44,39 +48,49 @@ def scatter_audio(audio: Optional[torch.Tensor], per_rank: int, samples: int, de
     return out
 
 
-def gather_tokens(tokens: torch.Tensor, lengths: torch.Tensor, dst: int = 0) -> Optional[List[List[int]]]:
-    """Gather per-rank (b, L) int32 tokens + (b,) lengths on `dst`; returns lists there, else None."""
+def gather_token_blocks(tokens: torch.Tensor, lengths: torch.Tensor,
+                        dst: int = 0) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+    """Gather per-rank (b, L) int32 tokens + (b,) lengths into (world*b, L) / (world*b,) device
+    tensors on `dst` (rank order = utterance order); None on the other ranks."""
     world = dist.get_world_size()
-    rank = dist.get_rank()
     tok = tokens.contiguous()
     ln = lengths.contiguous()
-    if rank == dst:
-        tok_all = [torch.empty_like(tok) for _ in range(world)]
-        len_all = [torch.empty_like(ln) for _ in range(world)]
-        dist.gather(tok, tok_all, dst=dst)
-        dist.gather(ln, len_all, dst=dst)
-        out = []
-        for t, n in zip(tok_all, len_all):
-            t, n = t.cpu(), n.cpu()
-            out.extend(t[i, : int(n[i])].tolist() for i in range(t.shape[0]))
-        return out
+    if dist.get_rank() == dst:
+        tok_all = torch.empty((world * tok.shape[0],) + tuple(tok.shape[1:]), dtype=tok.dtype, device=tok.device)
+        len_all = torch.empty((world * ln.shape[0],), dtype=ln.dtype, device=ln.device)
+        dist.gather(tok, list(tok_all.chunk(world, 0)), dst=dst)
+        dist.gather(ln, list(len_all.chunk(world, 0)), dst=dst)
+        return tok_all, len_all
     dist.gather(tok, None, dst=dst)
     dist.gather(ln, None, dst=dst)
     return None
 
 
+def gather_tokens(tokens: torch.Tensor, lengths: torch.Tensor, dst: int = 0) -> Optional[List[List[int]]]:
+    """Gather per-rank (b, L) int32 tokens + (b,) lengths on `dst`; returns lists there, else None."""
+    blocks = gather_token_blocks(tokens, lengths, dst)
+    if blocks is None:
+        return None
+    t, n = blocks[0].cpu(), blocks[1].cpu()
+    return [t[i, : int(n[i])].tolist() for i in range(t.shape[0])]
+
+
 def transcribe_sharded(step: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],
                        audio: Optional[torch.Tensor], batch: int, samples: int, device: torch.device,
-                       src: int = 0) -> Optional[List[List[int]]]:
+                       src: int = 0, shard: Optional[torch.Tensor] = None, as_lists: bool = True):
     """Scatter `batch` clips from `src`, run `step(shard) -> (tokens, lengths)` on every rank,
-    gather the token lists on `src`.  `batch` must divide by the world size (equal shards:
-    the model has no padding masks, so utterances are never padded to a common length)."""
+    gather the results on `src`: token lists, or with as_lists=False the (batch, L) / (batch,)
+    device tensors.  `batch` must divide by the world size (equal shards: the model has no
+    padding masks, so utterances are never padded to a common length).  shard: the buffer to
+    scatter into (a GraphedTranscriber's static input; see graphed_step)."""
     world = dist.get_world_size()
     if batch % world:
         raise ValueError(f"batch {batch} must be a multiple of the world size {world}")
-    shard = scatter_audio(audio, batch // world, samples, device, src)
+    shard = scatter_audio(audio, batch // world, samples, device, src, out=shard)
     tokens, lengths = step(shard)
-    return gather_tokens(tokens, lengths, src)
+    if as_lists:
+        return gather_tokens(tokens, lengths, src)
+    return gather_token_blocks(tokens, lengths, src)
 
 
 def hip_step(model) -> Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]:
@@ -85,4 +99,16 @@ def hip_step(model) -> Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor
 
     def step(shard: torch.Tensor):
         return audio_to_token_ids(model, shard)
+    return step
+
+
+def graphed_step(tr) -> Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]:
+    """The MI355X step as HIP graph replays of a GraphedTranscriber; the shard must be the
+    transcriber's own input buffer (pass shard=tr.audio to transcribe_sharded)."""
+
+    def step(shard: torch.Tensor):
+        if shard.data_ptr() != tr.audio.data_ptr():
+            raise ValueError("graphed_step: scatter into the transcriber's input (shard=tr.audio)")
+        tr.step()
+        return tr.tokens, tr.lengths
     return step

@@ -482,14 +482,24 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     return out.view(logits.shape[:-1])
 
 
-def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, timestamps: bool = False):
-    """Device-side greedy CTC collapse of (B, L) int32 predictions."""
+def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, timestamps: bool = False,
+                 out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """Device-side greedy CTC collapse of (B, L) int32 predictions.  out = (tokens (B, L),
+    lengths (B,)): contiguous int32 buffers to write into (e.g. row slices of a graph's
+    static output)."""
     if pred.device.type != "cuda" or pred.dtype != torch.int32:
         raise TypeError("ctc_collapse: expected a cuda int32 tensor")
     pred = pred.contiguous()
     B, Lq = pred.shape
-    toks = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
-    lens = torch.empty((B,), device=pred.device, dtype=torch.int32)
+    if out is None:
+        toks = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
+        lens = torch.empty((B,), device=pred.device, dtype=torch.int32)
+    else:
+        toks, lens = out
+        for n, t, shape in (("tokens", toks, (B, Lq)), ("lengths", lens, (B,))):
+            if (t.device != pred.device or t.dtype != torch.int32 or tuple(t.shape) != shape
+                    or not t.is_contiguous()):
+                raise ValueError(f"ctc_collapse: out {n} must be a contiguous int32 {shape} tensor on {pred.device}")
     st = en = None
     if timestamps:
         st = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)

@@ -25,14 +25,16 @@ from .model import VELOCITYASR
 FUSED_ARGMAX = os.environ.get("VASR_FUSED_ARGMAX", "1") != "0"
 
 
-def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(B, S) float32 HIP audio -> (tokens (B, L) int32, lengths (B,) int32), all on the device."""
+def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0,
+                       out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(B, S) float32 HIP audio -> (tokens (B, L) int32, lengths (B,) int32), all on the device.
+    out = (tokens, lengths) buffers to write the collapsed result into."""
     mel = mel_on_device(audio, SAMPLE_RATE, N_FFT, HOP_LENGTH, model.config.mel_bins)
     if FUSED_ARGMAX:
         pred = model.token_ids(mel)  # CTC head GEMM with the row argmax fused: no logits in HBM
     else:
         pred = ops.argmax(model(mel))
-    toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False)
+    toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False, out=out)
     return toks, lens
 
 
@@ -41,16 +43,30 @@ def token_lists(toks: torch.Tensor, lens: torch.Tensor) -> List[List[int]]:
     return [t[b, : n[b]].tolist() for b in range(t.shape[0])]
 
 
+def _model_fingerprint(model: torch.nn.Module):
+    """(tensor, data_ptr, version) of every parameter and buffer: a captured graph holds raw
+    pointers to them and to the derived weight layouts built from them (split-bf16 planes,
+    fake-quantized copies, [x_proj; dt_proj]), which are rebuilt -- and the old ones freed --
+    when a parameter changes."""
+    return [(t, t.data_ptr(), t._version) for t in list(model.parameters()) + list(model.buffers())]
+
+
 class GraphedTranscriber:
     """Fixed-shape (B, S) audio -> tokens step captured once in HIP graphs.
 
     ``audio`` is the static input buffer (write new clips into it, or use it as-is for
-    resident benchmark inputs); ``step()`` replays; ``tokens`` / ``lengths`` are the static
-    outputs.  With ``streams > 1`` the batch is split into that many utterance groups, each
-    captured in its own graph and replayed on its own HIP stream: the groups are independent
-    (no padding masks, per-utterance statistics), so results are bitwise those of one graph,
-    while the VALU-bound scan of one group overlaps the MFMA-bound GEMMs of another on the
-    same CUs (separate pipes).
+    resident benchmark inputs); ``step()`` replays; ``tokens`` (B, L) int32 and ``lengths``
+    (B,) int32 are the static outputs, refreshed by every replay.  With ``streams > 1`` the
+    batch is split into that many utterance groups, each captured in its own graph and
+    replayed on its own HIP stream; every group's collapse writes its rows of the shared
+    outputs.  The groups are independent (no padding masks, per-utterance statistics), so
+    results are bitwise those of one graph, while the VALU-bound scan of one group overlaps
+    the MFMA-bound GEMMs of another on the same CUs (separate pipes).
+
+    The graphs are tied to the model's parameters as they were at capture: ``step()`` raises
+    if any parameter or buffer was replaced or modified in place since (build a new
+    transcriber), and the derived weight layouts the graphs read are pinned for the
+    transcriber's lifetime so replay never reads freed memory.
     """
 
     def __init__(self, model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
@@ -61,9 +77,14 @@ class GraphedTranscriber:
         if batch % streams:
             raise ValueError("batch must divide by the number of streams")
         self.audio = torch.zeros((batch, samples), device=dev, dtype=torch.float32)
+        frames = samples // HOP_LENGTH + 1
+        L = model.get_output_length(frames)
+        self.tokens = torch.zeros((batch, L), device=dev, dtype=torch.int32)
+        self.lengths = torch.zeros((batch,), device=dev, dtype=torch.int32)
         g = batch // streams
         self.streams = [torch.cuda.Stream(dev) for _ in range(streams)]
         views = [self.audio[i * g:(i + 1) * g] for i in range(streams)]
+        outs = [(self.tokens[i * g:(i + 1) * g], self.lengths[i * g:(i + 1) * g]) for i in range(streams)]
         main = torch.cuda.current_stream(dev)
         for st, v in zip(self.streams, views):
             st.wait_stream(main)
@@ -71,21 +92,25 @@ class GraphedTranscriber:
                 for _ in range(warmup):  # builds the cached weight layouts before capture
                     audio_to_token_ids(model, v)
             main.wait_stream(st)
+        self._fingerprint = _model_fingerprint(model)
+        # pin every derived layout the graphs will read (they stay alive with the transcriber)
+        self._pinned = [dict(m.__dict__.get("_vasr_prepared", {})) for m in model.modules()]
+        self._pinned += [dict(ops._splits), dict(ops._f32_copies)]
         self.graphs = []
-        outs = []
-        for st, v in zip(self.streams, views):
+        for st, v, o in zip(self.streams, views, outs):
             gr = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gr, stream=st):
-                outs.append(audio_to_token_ids(model, v))
+                audio_to_token_ids(model, v, out=o)
             self.graphs.append(gr)
-        self.group_outputs = outs
-        if streams == 1:
-            self.tokens, self.lengths = outs[0]
-        else:
-            self.tokens = torch.cat([o[0] for o in outs], 0)  # snapshot; refresh with collect()
-            self.lengths = torch.cat([o[1] for o in outs], 0)
+
+    def _check_params(self) -> None:
+        for t, p, v in self._fingerprint:
+            if t.data_ptr() != p or t._version != v:
+                raise RuntimeError("GraphedTranscriber: the model's parameters changed after capture "
+                                   "(the graphs read the old weights); build a new GraphedTranscriber")
 
     def step(self) -> None:
+        self._check_params()
         main = torch.cuda.current_stream(self.device)
         for st, gr in zip(self.streams, self.graphs):
             st.wait_stream(main)
@@ -95,7 +120,5 @@ class GraphedTranscriber:
             main.wait_stream(st)
 
     def collect(self):
-        """(tokens, lengths) of the last step, concatenated over the stream groups."""
-        if len(self.graphs) == 1:
-            return self.tokens, self.lengths
-        return (torch.cat([o[0] for o in self.group_outputs], 0), torch.cat([o[1] for o in self.group_outputs], 0))
+        """(tokens, lengths) of the last step (the static outputs)."""
+        return self.tokens, self.lengths
