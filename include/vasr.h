@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 5
+#define VASR_ABI_VERSION 7
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -173,6 +173,34 @@ int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t l
                       const float* bc, int64_t ld_bc, const float* A2, const float* D,
                       float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
                       void* stream);
+
+/* Chunk-parallel form of modes 0 and 2 for small launches (one utterance at a time, as
+ * scripts/transcribe.py:69-78 and evaluate.py:91-98 run the model): time is cut at the
+ * streaming kernel's 16-step chunks; pass 1 forms each chunk's up-sweep composite, pass 2
+ * the composites of aligned blocks of 2^k chunks (the entries of the streaming kernel's
+ * chunk-level stack), pass 3 folds each chunk's prefix from them and runs the chunk's tree
+ * with the y reduction and gate.  Same float
+ * operations as vasr_ssm_scan_f32 with the same lane layout: bitwise equal outputs.
+ * workspace: >= vasr_ssm_scan_workspace_floats(B, L, Di, N) floats, 16-byte aligned. */
+int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,
+                              const float* bc, int64_t ld_bc, const float* A2, const float* D,
+                              float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
+                              float* workspace, int64_t workspace_floats, void* stream);
+int64_t vasr_ssm_scan_workspace_floats(int B, int L, int Di, int N);
+
+/* ------------------------------------------------------------------ audio I/O (host)
+ * load_audio (audio.py:22-62) without torchaudio.  Host functions on host memory (the only
+ * entry points here that are not device work): they produce the waveform the front end reads.
+ * vasr_flac_decode: a FLAC stream (torchaudio.load's FLAC path, audio.py:47) -> channel-major
+ *   (channels, samples) float32 scaled by 2^(bits-1); out = NULL queries the sizes.  Frame
+ *   CRCs are checked; errors return VASR_EINVAL with vasr_last_error().
+ * vasr_resample_f32: torchaudio.transforms.Resample(orig, new) defaults (sinc_interp_hann,
+ *   lowpass_filter_width 6, rolloff 0.99; audio.py:54-56), vasr_resample_length() outputs. */
+int vasr_flac_decode(const uint8_t* data, int64_t n, float* out, int64_t out_cap, int* channels,
+                     int* sample_rate, int* bits, int64_t* samples);
+int64_t vasr_resample_length(int64_t n, int orig_sr, int new_sr);
+int vasr_resample_f32(const float* x, int channels, int64_t n, int64_t ld_x, int orig_sr, int new_sr,
+                      float* y, int64_t ld_y);
 
 /* ------------------------------------------------------------------ mel front end
  * compute_mel_spectrogram (audio.py:65-143) is three launches:

@@ -202,14 +202,15 @@ __device__ __forceinline__ f2 exp2v(f2 v) {
 
 // The kernel body for each lane layout (scan_body.inc): npl4 = 4 state indices per lane
 // (G = N/4 lanes per channel), npl2 = 2 per lane (twice the waves for the same work).
-namespace npl4 {
-constexpr int NPL = 4;
-#include "scan_body.inc"
-}  // namespace npl4
+// (npl2 first: the chunk-parallel launcher of either layout uses npl2's block-level kernel)
 namespace npl2 {
 constexpr int NPL = 2;
 #include "scan_body.inc"
 }  // namespace npl2
+namespace npl4 {
+constexpr int NPL = 4;
+#include "scan_body.inc"
+}  // namespace npl4
 
 }  // namespace
 }  // namespace vasr
@@ -251,4 +252,55 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
         default: set_error("vasr_ssm_scan_f32: state dim N=%d not supported (16, 32, 64)", N); return VASR_EUNSUPPORTED;
     }
 #undef VASR_SCAN_N
+}
+
+VASR_API int64_t vasr_ssm_scan_workspace_floats(int B, int L, int Di, int N) {
+    if (B <= 0 || L <= 0 || Di <= 0 || N <= 0) return 0;
+    return 4 * (int64_t)B * ((L + 15) / 16) * Di * N;  // two arrays of [B][2 * nchunks][Di][N]
+}
+
+VASR_API int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,
+                                       const float* bc, int64_t ld_bc, const float* A2, const float* D, float* out,
+                                       int64_t ld_out, int B, int L, int Di, int N, int mode, float* workspace,
+                                       int64_t workspace_floats, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(xz && dt && bc && A2 && D && out, "vasr_ssm_scan_chunked_f32: null pointer");
+    VASR_CHECK_ARG(mode == 0 || mode == 2, "vasr_ssm_scan_chunked_f32: mode must be 0 or 2 (tree modes)");
+    VASR_CHECK_ARG(B >= 0 && L >= 0 && L <= 8192 && Di > 0, "vasr_ssm_scan_chunked_f32: bad shape B=%d L=%d Di=%d", B,
+                   L, Di);
+    VASR_CHECK_ARG(ld_xz % 4 == 0 && ld_dt % 4 == 0 && ld_bc % 4 == 0 && Di % 4 == 0,
+                   "vasr_ssm_scan_chunked_f32: leading dims and Di must be multiples of 4");
+    VASR_CHECK_ARG(ld_xz >= 2 * Di && ld_dt >= Di && ld_bc >= 2 * N && ld_out >= Di,
+                   "vasr_ssm_scan_chunked_f32: leading dims too small");
+    VASR_CHECK_ARG(((reinterpret_cast<uintptr_t>(xz) | reinterpret_cast<uintptr_t>(dt) |
+                     reinterpret_cast<uintptr_t>(bc) | reinterpret_cast<uintptr_t>(workspace)) & 15) == 0,
+                   "vasr_ssm_scan_chunked_f32: inputs and workspace must be 16-byte aligned");
+    if (B == 0 || L == 0) return VASR_OK;
+    const int64_t need = vasr_ssm_scan_workspace_floats(B, L, Di, N);
+    VASR_CHECK_ARG(workspace != nullptr && workspace_floats >= need,
+                   "vasr_ssm_scan_chunked_f32: workspace of %lld floats, %lld needed", (long long)workspace_floats,
+                   (long long)need);
+    VASR_CHECK_ARG(((int64_t)Di * N / 2) % 16 == 0 && (L + 15) / 16 - 1 <= 511,
+                   "vasr_ssm_scan_chunked_f32: needs Di * N / 2 divisible by 16 and L <= 8192");
+    float* ws_a = workspace;
+    float* ws_b = workspace + need / 2;
+    hipStream_t s = as_stream(stream);
+    // lane layout: 4 state indices per lane (the chunk-parallel grid has waves enough; 2 per lane
+    // measured slower: 40.0 vs 35.9 us at B = 1, L = 501 and 43.4 vs 37.7 at L = 1501);
+    // VASR_SCAN_NPL=2 forces the other (outputs are bitwise those of the streaming kernel with
+    // the same layout; the layouts differ in the order of the y = sum_n h C partial sums)
+    const char* npl_s = std::getenv("VASR_SCAN_NPL");
+    const bool two = npl_s && std::atoi(npl_s) == 2;
+#define VASR_SCAN_C(NS, NN)                                                                                         \
+    (mode == 0 ? NS::launch_chunked_n<NN, 0>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, ws_a,   \
+                                             ws_b, s)                                                             \
+               : NS::launch_chunked_n<NN, 2>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, ws_a,   \
+                                             ws_b, s))
+    switch (N) {
+        case 16: return two ? VASR_SCAN_C(npl2, 16) : VASR_SCAN_C(npl4, 16);
+        case 32: return two ? VASR_SCAN_C(npl2, 32) : VASR_SCAN_C(npl4, 32);
+        case 64: return two ? VASR_SCAN_C(npl2, 64) : VASR_SCAN_C(npl4, 64);
+        default: set_error("vasr_ssm_scan_chunked_f32: state dim N=%d not supported (16, 32, 64)", N); return VASR_EUNSUPPORTED;
+    }
+#undef VASR_SCAN_C
 }

@@ -101,27 +101,69 @@ def write_wav(path: str, audio, sample_rate: int = SAMPLE_RATE) -> None:
         f.write(b"RIFF" + len(riff).to_bytes(4, "little") + riff)
 
 
+def _read_flac(path: str) -> Tuple[torch.Tensor, int]:
+    """FLAC file -> ((channels, samples) float32 scaled by 2^(bits-1), sample rate), decoded by
+    the library's host decoder (vasr_flac_decode; frame CRCs checked)."""
+    import ctypes
+    with open(path, "rb") as f:
+        data = f.read()
+    lib = _lib.lib()
+    ch, sr, bits, ns = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    buf = ctypes.create_string_buffer(data, len(data))
+    args = (ctypes.byref(ch), ctypes.byref(sr), ctypes.byref(bits), ctypes.byref(ns))
+    rc = lib.vasr_flac_decode(ctypes.addressof(buf), len(data), None, 0, *args)
+    if rc != 0:
+        raise ValueError(f"{path}: {lib.vasr_last_error().decode(errors='replace')}")
+    out = np.empty((ch.value, ns.value), np.float32)
+    _lib.check(lib.vasr_flac_decode(ctypes.addressof(buf), len(data), out.ctypes.data, out.size, *args),
+               "vasr_flac_decode")
+    return torch.from_numpy(out), sr.value
+
+
+def resample(waveform: torch.Tensor, orig_freq: int, new_freq: int) -> torch.Tensor:
+    """torchaudio.transforms.Resample(orig_freq, new_freq) with its defaults (sinc_interp_hann,
+    lowpass_filter_width 6, rolloff 0.99) on a host (..., samples) float32 waveform, by the
+    library's host resampler (vasr_resample_f32).  Equality with torchaudio is unpinned
+    (torchaudio is not installed here): same kernel formula, float64 accumulation."""
+    x = np.ascontiguousarray(waveform.detach().cpu().numpy(), dtype=np.float32)
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, x.shape[-1])
+    n = x2.shape[1]
+    lib = _lib.lib()
+    m = int(lib.vasr_resample_length(n, int(orig_freq), int(new_freq)))
+    y = np.empty((x2.shape[0], m), np.float32)
+    if n and x2.shape[0]:
+        _lib.check(lib.vasr_resample_f32(x2.ctypes.data, x2.shape[0], n, n, int(orig_freq), int(new_freq), y.ctypes.data,
+                                         m), "vasr_resample_f32")
+    return torch.from_numpy(y.reshape(*lead, m))
+
+
 def load_audio(path: str, sample_rate: int = SAMPLE_RATE, mono: bool = True) -> torch.Tensor:
     """Load audio and resample (reference audio.py:22-62).
 
-    Uses torchaudio when it is installed (same as the reference); otherwise reads PCM WAV
-    with the standard library.  Returns (samples,) for mono or (channels, samples).
+    Uses torchaudio when it is installed (same as the reference); otherwise reads WAV with the
+    standard library and FLAC (LibriSpeech's format) with the library's host decoder, and
+    resamples with the host resampler that follows torchaudio's Resample defaults.  Returns
+    (samples,) for mono or (channels, samples), float32 on the host like the reference.
     """
     try:
-        import torchaudio  # noqa: F401
+        import torchaudio
         waveform, sr = torchaudio.load(path)
+        resampler = lambda w, a, b: torchaudio.transforms.Resample(a, b)(w)  # noqa: E731
     except ImportError:
-        if not path.lower().endswith(".wav"):
-            raise ImportError("torchaudio is required for non-WAV audio. Install with: pip install torchaudio")
-        waveform, sr = _read_wav(path)
+        low = path.lower()
+        if low.endswith(".wav"):
+            waveform, sr = _read_wav(path)
+        elif low.endswith(".flac"):
+            waveform, sr = _read_flac(path)
+        else:
+            raise ImportError("torchaudio is required for audio formats other than WAV and FLAC. "
+                              "Install with: pip install torchaudio")
+        resampler = resample
     if mono and waveform.size(0) > 1:
         waveform = waveform.mean(dim=0, keepdim=True)
     if sr != sample_rate:
-        try:
-            import torchaudio
-        except ImportError:
-            raise ImportError(f"resampling {sr} Hz -> {sample_rate} Hz needs torchaudio")
-        waveform = torchaudio.transforms.Resample(sr, sample_rate)(waveform)
+        waveform = resampler(waveform, sr, sample_rate)
     if mono:
         waveform = waveform.squeeze(0)
     return waveform

@@ -360,9 +360,26 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
     return y
 
 
+# Chunk-parallel tree scan (vasr_ssm_scan_chunked_f32, bitwise equal to the streaming kernel)
+# for launches under CHUNKED_MAX_WAVES waves of the streaming kernel (B * Di * N / 256; 768 on
+# 1024 SIMDs): one utterance at a time, as the reference's scripts feed the model.
+# VASR_SCAN_CHUNKED=0|1 forces the streaming / chunked form (read per call).
+CHUNKED_MAX_WAVES = 512
+
+
+def _use_chunked(B: int, Lq: int, Di: int, N: int, mode: int) -> bool:
+    if mode not in (0, 2) or Lq <= 16:
+        return False
+    env = os.environ.get("VASR_SCAN_CHUNKED")
+    if env is not None:
+        return env == "1"
+    return B * Di * N // 256 < CHUNKED_MAX_WAVES
+
+
 def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Tensor, D: torch.Tensor, B: int,
              Lq: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Gated selective scan.  xz (B*L, 2Di) [x|z], dt (B*L, Di), bc (B*L, 2N) [B|C] (row views)."""
+    """Gated selective scan.  xz (B*L, 2Di) [x|z], dt (B*L, Di), bc (B*L, 2N) [B|C] (row views).
+    Small launches of the tree modes take the chunk-parallel form (same results, bitwise)."""
     D = f32(D)
     for n, t in (("xz", xz), ("dt", dt), ("bc", bc), ("A2", A2), ("D", D)):
         _cuda_f32(f"ssm_scan.{n}", t)
@@ -374,11 +391,23 @@ def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Ten
     if out is None:
         out = torch.empty((M, Di), device=xz.device, dtype=torch.float32)
     _, _, ld_out = _rows("ssm_scan.out", out)
+    N = A2.numel()
+    chunked = _use_chunked(B, Lq, Di, N, int(mode))
+    ws = None
+    if chunked:
+        nws = int(L.lib().vasr_ssm_scan_workspace_floats(B, Lq, Di, N))
+        ws = torch.empty(nws, device=xz.device, dtype=torch.float32)
     ev = _t0("ssm_scan")
-    check(L.lib().vasr_ssm_scan_f32(xz.data_ptr(), ld_xz, dt.data_ptr(), ld_dt, bc.data_ptr(), ld_bc, A2.data_ptr(),
-                                    D.data_ptr(), out.data_ptr(), ld_out, B, Lq, Di, A2.numel(), int(mode),
-                                    stream_of(xz)), "vasr_ssm_scan_f32")
-    _t1("ssm_scan", ev, dict(B=B, L=Lq, Di=Di, N=A2.numel(), mode=int(mode)))
+    if chunked:
+        check(L.lib().vasr_ssm_scan_chunked_f32(xz.data_ptr(), ld_xz, dt.data_ptr(), ld_dt, bc.data_ptr(), ld_bc,
+                                                A2.data_ptr(), D.data_ptr(), out.data_ptr(), ld_out, B, Lq, Di, N,
+                                                int(mode), ws.data_ptr(), ws.numel(), stream_of(xz)),
+              "vasr_ssm_scan_chunked_f32")
+    else:
+        check(L.lib().vasr_ssm_scan_f32(xz.data_ptr(), ld_xz, dt.data_ptr(), ld_dt, bc.data_ptr(), ld_bc, A2.data_ptr(),
+                                        D.data_ptr(), out.data_ptr(), ld_out, B, Lq, Di, N, int(mode),
+                                        stream_of(xz)), "vasr_ssm_scan_f32")
+    _t1("ssm_scan", ev, dict(B=B, L=Lq, Di=Di, N=N, mode=int(mode), chunked=chunked))
     return out
 
 
