@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 7
+#define VASR_ABI_VERSION 8
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -187,6 +187,24 @@ int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const float* dt, i
                               float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
                               float* workspace, int64_t workspace_floats, void* stream);
 int64_t vasr_ssm_scan_workspace_floats(int B, int L, int Di, int N);
+
+/* ------------------------------------------------------------------ SSMBlock tail, fused
+ * The tail of SSMBlock._forward_impl (ssm.py:415-425) in one launch for d_model D = 192 and
+ * FFN width / d_inner E = 384:
+ *   x1 = g @ Wo^T + x;  h = LayerNorm(x1; ln_w, ln_b, ln_eps);  f = gelu(h @ W1^T + b1);
+ *   out = f @ W2^T + b2 + x1
+ * with g (M, E) the gated scan output (row stride ldg), x (M, D) the block input, Wo = out_proj
+ * (D x E, ssm.py:90), W1 = ffn.0 (E x D), W2 = ffn.3 (D x E) (ssm.py:394-400), each given as
+ * vasr_split_weights16_bf16x3 planes.  x1 and f never leave the chip.  fp32-accurate (split
+ * bf16 products, as vasr_linear_x3_f32). */
+int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo16,
+                            const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                            const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
+                            int M, int D, int E, void* stream);
+/* Split-bf16 planes of a (N, K) fp32 weight in the fragment layout of v_mfma_f32_16x16x32_bf16
+ * ([ceil(N/16)][ceil(K/32)][3][64][8] bf16), vasr_split_weights16_elems(N, K) uint16 elements. */
+int vasr_split_weights16_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
+int64_t vasr_split_weights16_elems(int N, int K);
 
 /* ------------------------------------------------------------------ audio I/O (host)
  * load_audio (audio.py:22-62) without torchaudio.  Host functions on host memory (the only

@@ -1,0 +1,87 @@
+"""Fused SSMBlock tail (vasr_ssm_block_tail_f32): out_proj + residual -> LayerNorm_2 -> FFN1 +
+GELU -> FFN2 + residual in one kernel (reference ssm.py:415-425).
+
+Checked against an fp64 numpy restatement of the same four steps (fp32 parity bar: the
+split-bf16 products are fp32-accurate), against the unfused launches, and at model level by
+the golden-pinned parity suite (tests/test_gpu_parity.py), which runs with the fused tail (the
+default)."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _gelu(x):
+    from scipy.special import erf
+    return 0.5 * x * (1.0 + erf(x / math.sqrt(2.0)))
+
+
+def _params(seed, D=192, E=384):
+    rng = np.random.default_rng(seed)
+    f = lambda *s, sc=1.0: (rng.standard_normal(s) * sc).astype(np.float32)  # noqa: E731
+    return dict(wo=f(D, E, sc=1 / math.sqrt(E)), ln_w=(1 + 0.1 * rng.standard_normal(D)).astype(np.float32),
+                ln_b=f(D, sc=0.1), w1=f(E, D, sc=1 / math.sqrt(D)), b1=f(E, sc=0.1),
+                w2=f(D, E, sc=1 / math.sqrt(E)), b2=f(D, sc=0.1))
+
+
+def _ref(g, x, P, eps=1e-5):
+    g, x = g.astype(np.float64), x.astype(np.float64)
+    x1 = g @ P["wo"].astype(np.float64).T + x
+    mu = x1.mean(-1, keepdims=True)
+    var = ((x1 - mu) ** 2).mean(-1, keepdims=True)
+    h = (x1 - mu) / np.sqrt(var + eps) * P["ln_w"] + P["ln_b"]
+    f = _gelu(h @ P["w1"].astype(np.float64).T + P["b1"])
+    return f @ P["w2"].astype(np.float64).T + P["b2"] + x1
+
+
+def _run(g, x, P, ldg=None):
+    from velocity_asr import ops
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    gt = t(g)
+    if ldg is not None:
+        big = torch.zeros((g.shape[0], ldg), device=DEV)
+        big[:, :g.shape[1]] = gt
+        gt = big[:, :g.shape[1]]
+    return ops.ssm_block_tail(gt, t(x), t(P["wo"]), t(P["ln_w"]), t(P["ln_b"]), 1e-5, t(P["w1"]), t(P["b1"]),
+                              t(P["w2"]), t(P["b2"])).cpu().numpy()
+
+
+@pytest.mark.parametrize("M", [1, 16, 31, 32, 33, 100, 501, 8016])
+def test_tail_matches_fp64(M):
+    rng = np.random.default_rng(M)
+    P = _params(7)
+    g = rng.standard_normal((M, 384)).astype(np.float32)
+    x = rng.standard_normal((M, 192)).astype(np.float32)
+    got = _run(g, x, P)
+    ref = _ref(g, x, P)
+    np.testing.assert_allclose(got, ref, atol=2e-5 * max(1.0, np.abs(ref).max()), rtol=2e-5)
+
+
+def test_tail_strided_input():
+    rng = np.random.default_rng(3)
+    P = _params(8)
+    g = rng.standard_normal((77, 384)).astype(np.float32)
+    x = rng.standard_normal((77, 192)).astype(np.float32)
+    np.testing.assert_allclose(_run(g, x, P, ldg=768), _ref(g, x, P), atol=1e-4, rtol=2e-5)
+
+
+def test_fused_block_equals_unfused_launches(monkeypatch):
+    """SSMBlock.forward with the fused tail vs the four launches it replaces (same model
+    weights): equal to the fp32 rounding of the two accumulation groupings."""
+    import velocity_asr as va
+    from velocity_asr import synthetic as S
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    blk = m.to(DEV).eval().local_ssm.layers[3]
+    x = torch.from_numpy(np.random.default_rng(5).standard_normal((3, 250, 192)).astype(np.float32)).to(DEV)
+    monkeypatch.setenv("VASR_FUSED_TAIL", "1")
+    fused = blk(x)
+    monkeypatch.setenv("VASR_FUSED_TAIL", "0")
+    plain = blk(x)
+    torch.testing.assert_close(fused, plain, atol=3e-5, rtol=1e-5)

@@ -1,0 +1,360 @@
+// The tail of an SSMBlock as ONE kernel (reference ssm.py:415-425, SSMBlock._forward_impl):
+//
+//     x1  = out_proj(g) + x               (ssm.py:130 out_proj, :419 residual)
+//     h   = LayerNorm_2(x1)               (:422)
+//     f   = GELU(ffn.0(h))                (:394-397)
+//     out = ffn.3(f) + x1                 (:398-400, :425)
+//
+// for D = 192, E = 384 (d_model, FFN width / d_inner).  The unfused form is three GEMM launches
+// plus a LayerNorm launch that write and re-read x1 (D floats per token) and the FFN
+// intermediate (E floats per token) through HBM; here one workgroup owns 32 token rows and
+// keeps everything on chip: the scan output tile g (32 x 384 fp32) staged once by LDS-DMA,
+// x1 in registers (and in LDS for the LayerNorm), h and f in LDS as the next product's A
+// operand.  HBM traffic per token: g in (1536 B), x in (768 B), out (768 B) -- the weights
+// (1.3 MB of split planes for the three matrices) stream from L2, the same for every row tile.
+//
+// Arithmetic: the split-bf16 fp32 GEMM of gemm_x3.hip (x = hi + mid + lo, six bf16 products,
+// small terms first), on v_mfma_f32_16x16x32_bf16 (K = 32 per instruction); LayerNorm with the
+// float operations of vasr_layer_norm_f32; the same bias / GELU / residual epilogues.  The
+// result is an fp32 computation of the block tail; it differs from the unfused launches only
+// in the MFMA accumulation grouping (32 k per instruction here, 16 there).
+//
+// Work decomposition: 4 waves (one per SIMD), 32 token rows; each output 32 x 192 is 2 x 12
+// tiles of 16 x 16 and wave w owns column tiles 3w .. 3w + 2 of both row tiles (FFN1's 32 x 384
+// runs as two 192-column halves with the same map), so no two waves need the same weight
+// fragment: weights go global -> VGPRs straight from their fragment-native split planes, each
+// wave prefetching PD 32-k steps ahead (the 36 steps of the three products form one stream:
+// prefetch runs across the product boundaries).  A operands sit in LDS already split into
+// their three bf16 planes (each element split once per block, not once per wave), 16-B chunk c
+// of row r at c ^ (r & 15) (384-wide) or c ^ (r & 7) (192-wide): conflict-free fragment reads.
+// LDS: 72 KiB for the 384-wide planes (g, then f; the fp32 x1 scratch of the LayerNorm lives
+// there in between) + 36 KiB for the 192-wide planes of h.
+#include "gemm_split.h"
+
+namespace vasr {
+namespace {
+
+using gemm::bf16x8;
+using gemm::split8;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int TD = 192;          // d_model
+constexpr int TE = 384;          // FFN width = d_inner
+constexpr int TBM = 32;          // token rows per workgroup
+constexpr int TWAVES = 4;
+constexpr int NSTAGES = 36;      // out_proj 12 k-steps, FFN1 2 halves x 6, FFN2 12
+constexpr int PD = 3;            // weight prefetch distance (steps)
+constexpr int RING = PD + 1;
+constexpr int PLANE_E = TBM * TE * 2;  // one bf16 plane of a 384-wide A tile (24 KiB)
+constexpr int PLANE_D = TBM * TD * 2;  // one bf16 plane of a 192-wide A tile (12 KiB)
+
+// byte offset of bf16 element (r, col) in one plane: 8-element (16-B) chunks, swizzled
+template <int WIDTH>
+__device__ __forceinline__ int poff(int r, int col) {
+    constexpr int SW = WIDTH == TE ? 15 : 7;
+    return r * WIDTH * 2 + ((((col >> 3) ^ (r & SW))) << 4) + ((col & 7) << 1);
+}
+
+struct TailParams {
+    const float* g;
+    int64_t ldg;
+    const float* x;
+    int64_t ldx;
+    const uint16_t* wo;  // out_proj (D x E) in the 16x16x32 fragment layout, 3 planes
+    const float* ln_w;
+    const float* ln_b;
+    float ln_eps;
+    const uint16_t* w1;  // ffn.0 (E x D)
+    const float* b1;
+    const uint16_t* w2;  // ffn.3 (D x E)
+    const float* b2;
+    float* out;
+    int64_t ldo;
+    int M;
+};
+
+struct TailCtx {
+    const TailParams& P;
+    char* R;   // 384-wide planes (g, f) / fp32 x1 scratch
+    char* H;   // 192-wide planes (h)
+    int lane, wave, r, q, m0;
+    floatx4 acc[2][3];
+    bf16x8 w[RING][3][3];  // [ring slot][column tile][plane]
+    float x1[2][3][4];     // residual x, then x1 = out_proj(g) + x
+    float bb1[2][3], bb2[3], lnw[3], lnb[3];
+};
+
+// weight fragments of step S for this wave: column tiles 3w .. 3w+2, three planes, from the
+// fragment layout [N/16][K/32][3][64][8]
+template <int S>
+__device__ __forceinline__ void load_w(TailCtx& c) {
+    const uint16_t* W;
+    int nt0, ks, KS;
+    if constexpr (S < 12) {
+        W = c.P.wo, nt0 = 0, ks = S, KS = TE / 32;
+    } else if constexpr (S < 24) {
+        W = c.P.w1, nt0 = 12 * ((S - 12) / 6), ks = (S - 12) % 6, KS = TD / 32;
+    } else {
+        W = c.P.w2, nt0 = 0, ks = S - 24, KS = TE / 32;
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int nt = nt0 + 3 * c.wave + t;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            c.w[S % RING][t][pl] =
+                *reinterpret_cast<const bf16x8*>(W + ((int64_t)(nt * KS + ks) * 3 + pl) * 512 + c.lane * 8);
+    }
+}
+
+__device__ __forceinline__ void split_store(char* plane0, int plane_bytes, int off, float v) {
+    __bf16 a, b, cc;
+    gemm::split1(v, a, b, cc);
+    *reinterpret_cast<__bf16*>(plane0 + off) = a;
+    *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = b;
+    *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = cc;
+}
+
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (prefetch stays in flight)
+    __builtin_amdgcn_s_barrier();
+}
+
+template <int S>
+__device__ __forceinline__ void tail_step(TailCtx& c) {
+    if constexpr (S + PD < NSTAGES) load_w<S + PD>(c);
+    // keep the prefetch where it is: without this fence the scheduler sinks the loads next to
+    // their use (to save registers) and the step then waits on them (measured: the weight
+    // stream then ran at a third of the L2 rate)
+    __builtin_amdgcn_sched_barrier(0);
+    // A fragments of both row tiles, three planes each
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+        const int row = 16 * tm + c.r;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            if constexpr (S < 12 || S >= 24) {
+                constexpr int ks = S < 12 ? S : S - 24;
+                a[tm][pl] = *reinterpret_cast<const bf16x8*>(c.R + pl * PLANE_E + row * TE * 2 +
+                                                             (((4 * ks + c.q) ^ (row & 15)) << 4));
+            } else {
+                constexpr int ks = (S - 12) % 6;
+                a[tm][pl] = *reinterpret_cast<const bf16x8*>(c.H + pl * PLANE_D + row * TD * 2 +
+                                                             (((4 * ks + c.q) ^ (row & 7)) << 4));
+            }
+        }
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {  // small terms first, then the leading hi * hi (as gemm_x3)
+            const bf16x8(&wf)[3] = c.w[S % RING][t];
+            floatx4 v = c.acc[tm][t];
+            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][2], wf[0], v, 0, 0, 0);
+            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[2], v, 0, 0, 0);
+            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[1], v, 0, 0, 0);
+            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[0], v, 0, 0, 0);
+            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[1], v, 0, 0, 0);
+            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[0], v, 0, 0, 0);
+            c.acc[tm][t] = v;
+        }
+
+    if constexpr (S == 11) {
+        // x1 = out_proj(g) + x (registers, kept for the final residual) -> fp32 scratch in R
+        // (the g planes are dead once every wave is past its last GEMM1 read)
+        lds_barrier();
+        float* xs = reinterpret_cast<float*>(c.R);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int col = 16 * (3 * c.wave + t) + c.r;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    c.x1[tm][t][i] = c.acc[tm][t][i] + c.x1[tm][t][i];
+                    xs[(16 * tm + 4 * c.q + i) * TD + col] = c.x1[tm][t][i];
+                }
+                c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        lds_barrier();
+        // h = LayerNorm_2(x1): one wave per row with vasr_layer_norm_f32's operations, each
+        // value split into the three planes of H
+#pragma unroll
+        for (int k = 0; k < TBM / TWAVES; ++k) {
+            const int rr = TBM / TWAVES * c.wave + k;
+            float v[3];
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                v[i] = xs[rr * TD + c.lane + 64 * i];
+                sum += v[i];
+            }
+            const float mean = wave_sum(sum) / (float)TD;
+            float qs = 0.f;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float d = v[i] - mean;
+                qs += d * d;
+            }
+            const float var = wave_sum(qs) / (float)TD;
+            const float rstd = 1.0f / sqrtf(var + c.P.ln_eps);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                split_store(c.H, PLANE_D, poff<TD>(rr, c.lane + 64 * i), __builtin_fmaf((v[i] - mean) * rstd, c.lnw[i], c.lnb[i]));
+        }
+        lds_barrier();  // h complete; the scratch in R is free for f
+    } else if constexpr (S == 17 || S == 23) {
+        // f = GELU(ffn.0(h) + b1), FFN1 column half hh, split into the planes of R
+        constexpr int hh = S == 17 ? 0 : 1;
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int col = TD * hh + 16 * (3 * c.wave + t) + c.r;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    split_store(c.R, PLANE_E, poff<TE>(16 * tm + 4 * c.q + i, col),
+                                gelu_fast(c.acc[tm][t][i] + c.bb1[hh][t]));
+                c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        if constexpr (S == 23) lds_barrier();  // f complete before FFN2 reads it
+    }
+    if constexpr (S + 1 < NSTAGES) tail_step<S + 1>(c);
+}
+
+__global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
+    __shared__ __attribute__((aligned(16))) char R[3 * PLANE_E];
+    __shared__ __attribute__((aligned(16))) char H[3 * PLANE_D];
+    TailCtx c{P, R, H};
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    c.r = c.lane & 15;
+    c.q = c.lane >> 4;
+    c.m0 = blockIdx.x * TBM;
+    // weights of the first PD steps, then the g tile (split once into R's planes), the residual
+    // x and the epilogue constants: all of these loads are in flight together
+    load_w<0>(c);
+    load_w<1>(c);
+    load_w<2>(c);
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int UNITS = TBM * TE / 8;  // 8-float chunks of the g tile
+#pragma unroll
+    for (int k = 0; k < UNITS / 256; ++k) {
+        const int u = threadIdx.x + 256 * k;
+        const int rr = u / (TE / 8), ch = u - rr * (TE / 8);
+        const float* src = P.g + (int64_t)min(c.m0 + rr, P.M - 1) * P.ldg + 8 * ch;
+        const float4 v0 = *reinterpret_cast<const float4*>(src);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        bf16x8 hi, mid, lo;
+        split8(v0, v1, hi, mid, lo);
+        const int off = rr * TE * 2 + ((ch ^ (rr & 15)) << 4);
+        *reinterpret_cast<bf16x8*>(R + off) = hi;
+        *reinterpret_cast<bf16x8*>(R + PLANE_E + off) = mid;
+        *reinterpret_cast<bf16x8*>(R + 2 * PLANE_E + off) = lo;
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int col = 16 * (3 * c.wave + t) + c.r;
+            c.bb2[t] = P.b2[col];
+            c.bb1[0][t] = P.b1[col];
+            c.bb1[1][t] = P.b1[TD + col];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = c.m0 + 16 * tm + 4 * c.q + i;
+                c.x1[tm][t][i] = row < P.M ? P.x[(int64_t)row * P.ldx + col] : 0.0f;
+            }
+            c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        c.lnw[i] = P.ln_w[c.lane + 64 * i];
+        c.lnb[i] = P.ln_b[c.lane + 64 * i];
+    }
+    lds_barrier();  // the g planes are complete
+    tail_step<0>(c);
+    // out = ffn.3(f) + b2 + x1
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int col = 16 * (3 * c.wave + t) + c.r;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = c.m0 + 16 * tm + 4 * c.q + i;
+                if (row < P.M) P.out[(int64_t)row * P.ldo + col] = (c.acc[tm][t][i] + c.bb2[t]) + c.x1[tm][t][i];
+            }
+        }
+}
+
+// Fragment layout of v_mfma_f32_16x16x32_bf16's B operand, three split planes:
+// [ceil(N/16)][Kp/32][3][64 lanes][8], lane l of (tile nt, step ks) holding
+// W[16 nt + (l & 15)][32 ks + 8 (l >> 4) + j]; zero outside N x K.
+__global__ void split_weights16_kernel(const float* __restrict__ W, int64_t ldw, int N, int K, int Kp,
+                                       uint16_t* __restrict__ out) {
+    const int64_t qd = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one thread per 8 k of one row
+    const int cpr = Kp / 8;
+    const int NT = (N + 15) / 16;
+    if (qd >= (int64_t)NT * 16 * cpr) return;
+    const int n = (int)(qd / cpr), k0 = (int)(qd % cpr) * 8;
+    bf16x8 hi, mid, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v = (n < N && k0 + j < K) ? W[(int64_t)n * ldw + k0 + j] : 0.0f;
+        __bf16 a, b, c;
+        gemm::split1(v, a, b, c);
+        hi[j] = a;
+        mid[j] = b;
+        lo[j] = c;
+    }
+    const int KS = Kp / 32;
+    const int ln = 16 * ((k0 % 32) / 8) + n % 16;
+    const int64_t base = ((int64_t)(n / 16) * KS + k0 / 32) * 3 * 512 + ln * 8;
+    *reinterpret_cast<bf16x8*>(out + base) = hi;
+    *reinterpret_cast<bf16x8*>(out + base + 512) = mid;
+    *reinterpret_cast<bf16x8*>(out + base + 1024) = lo;
+}
+
+}  // namespace
+}  // namespace vasr
+
+VASR_API int64_t vasr_split_weights16_elems(int N, int K) {
+    if (N <= 0 || K <= 0) return 0;
+    return 3 * (int64_t)((N + 15) / 16 * 16) * ((K + 31) / 32 * 32);
+}
+
+VASR_API int vasr_split_weights16_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(W && out, "vasr_split_weights16_bf16x3: null pointer");
+    VASR_CHECK_ARG(N > 0 && K > 0 && ldw >= K, "vasr_split_weights16_bf16x3: bad shape N=%d K=%d", N, K);
+    VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "vasr_split_weights16_bf16x3: out must be 16-B aligned");
+    const int Kp = (K + 31) / 32 * 32;
+    const int64_t n = (int64_t)((N + 15) / 16 * 16) * (Kp / 8);
+    hipLaunchKernelGGL(split_weights16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), W, ldw,
+                       N, K, Kp, out);
+    return launch_status("vasr_split_weights16_bf16x3");
+}
+
+VASR_API int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo16,
+                                     const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                                     const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
+                                     int M, int D, int E, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(g && x && wo16 && ln_w && ln_b && w1_16 && b1 && w2_16 && b2 && out,
+                   "vasr_ssm_block_tail_f32: null pointer");
+    VASR_CHECK_ARG(D == TD && E == TE, "vasr_ssm_block_tail_f32: built for d_model %d, FFN width %d (got %d, %d)", TD, TE,
+                   D, E);
+    VASR_CHECK_ARG(M >= 0 && ldg >= E && ldx >= D && ldo >= D && ldg % 4 == 0,
+                   "vasr_ssm_block_tail_f32: bad shape M=%d ldg=%lld ldx=%lld ldo=%lld", M, (long long)ldg,
+                   (long long)ldx, (long long)ldo);
+    VASR_CHECK_ARG(((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(wo16) |
+                     reinterpret_cast<uintptr_t>(w1_16) | reinterpret_cast<uintptr_t>(w2_16)) & 15) == 0,
+                   "vasr_ssm_block_tail_f32: g and the weight planes must be 16-byte aligned");
+    if (M == 0) return VASR_OK;
+    TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
+    hipLaunchKernelGGL(ssm_tail_kernel, dim3((M + TBM - 1) / TBM), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    return launch_status("vasr_ssm_block_tail_f32");
+}

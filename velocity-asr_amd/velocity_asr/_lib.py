@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -63,6 +63,10 @@ _SIGNATURES = {
     "vasr_ssm_scan_chunked_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5
                                   + [c_p, c_i64, c_p], ctypes.c_int),
     "vasr_ssm_scan_workspace_floats": ([ctypes.c_int] * 4, c_i64),
+    "vasr_ssm_block_tail_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
+                                + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
+    "vasr_split_weights16_bf16x3": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
+    "vasr_split_weights16_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_flac_decode": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p], ctypes.c_int),
     "vasr_resample_length": ([c_i64, ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_resample_f32": ([c_p, ctypes.c_int, c_i64, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_i64], ctypes.c_int),

@@ -148,6 +148,50 @@ def split_weights(w: torch.Tensor) -> torch.Tensor:
     return planes
 
 
+_splits16 = {}
+
+
+def split_weights16(w: torch.Tensor) -> torch.Tensor:
+    """Split-bf16 planes of a (N, K) fp32 weight in the v_mfma_f32_16x16x32_bf16 fragment
+    layout (the fused SSMBlock tail), built once per (tensor, version)."""
+    N, K, ldw = _rows("split16.w", w)
+    sig = (w.data_ptr(), w._version, N, K, ldw)
+    ent = _splits16.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == sig:
+        return ent[2]
+    planes = torch.empty(int(L.lib().vasr_split_weights16_elems(N, K)), device=w.device, dtype=torch.int16)
+    check(L.lib().vasr_split_weights16_bf16x3(w.data_ptr(), ldw, N, K, planes.data_ptr(), stream_of(w)),
+          "vasr_split_weights16_bf16x3")
+    key = id(w)
+    _splits16[key] = (weakref.ref(w, lambda _r, k=key: _splits16.pop(k, None)), sig, planes)
+    return planes
+
+
+def ssm_block_tail(g: torch.Tensor, x: torch.Tensor, wo: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor,
+                   ln_eps: float, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused SSMBlock tail (vasr_ssm_block_tail_f32): out = ffn(LN2(g Wo^T + x)) + (g Wo^T + x)
+    for g (M, 384) and x (M, 192) row views (d_model 192, FFN width 384)."""
+    for n, t in (("g", g), ("x", x), ("wo", wo), ("ln_w", ln_w), ("ln_b", ln_b), ("w1", w1), ("b1", b1),
+                 ("w2", w2), ("b2", b2)):
+        _cuda_f32(f"ssm_block_tail.{n}", t)
+    M, E, ldg = _rows("ssm_block_tail.g", g)
+    Mx, D, ldx = _rows("ssm_block_tail.x", x)
+    if Mx != M or tuple(wo.shape) != (D, E) or tuple(w1.shape) != (E, D) or tuple(w2.shape) != (D, E):
+        raise ValueError("ssm_block_tail: inconsistent shapes")
+    if out is None:
+        out = torch.empty((M, D), device=g.device, dtype=torch.float32)
+    _, _, ldo = _rows("ssm_block_tail.out", out)
+    ev = _t0("ssm_tail")
+    check(L.lib().vasr_ssm_block_tail_f32(g.data_ptr(), ldg, x.data_ptr(), ldx, split_weights16(wo).data_ptr(),
+                                          ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(), float(ln_eps),
+                                          split_weights16(w1).data_ptr(), b1.contiguous().data_ptr(),
+                                          split_weights16(w2).data_ptr(), b2.contiguous().data_ptr(), out.data_ptr(),
+                                          ldo, M, D, E, stream_of(g)), "vasr_ssm_block_tail_f32")
+    _t1("ssm_tail", ev, dict(M=M, D=D, E=E))
+    return out
+
+
 def pack_bf16(w: torch.Tensor) -> torch.Tensor:
     """One fragment-native bf16 plane (as int16 storage) of a (N, K) bf16 weight view."""
     N, K, ldw = _rows("pack.w", w)

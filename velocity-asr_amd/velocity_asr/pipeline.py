@@ -95,7 +95,7 @@ class GraphedTranscriber:
         self._fingerprint = _model_fingerprint(model)
         # pin every derived layout the graphs will read (they stay alive with the transcriber)
         self._pinned = [dict(m.__dict__.get("_vasr_prepared", {})) for m in model.modules()]
-        self._pinned += [dict(ops._splits), dict(ops._f32_copies)]
+        self._pinned += [dict(ops._splits), dict(ops._splits16), dict(ops._f32_copies)]
         self.graphs = []
         for st, v, o in zip(self.streams, views, outs):
             gr = torch.cuda.CUDAGraph()
