@@ -201,6 +201,15 @@ int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x, int64_t
                             const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
                             const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
                             int M, int D, int E, void* stream);
+/* The same tail for the bf16 model (C3): weights as one bf16 plane (vasr_pack_weights16_bf16 of
+ * the bf16 parameters), activations rounded to bf16 at the MFMA input, fp32 accumulation and
+ * fp32 LayerNorm / bias / GELU / residual -- the arithmetic of vasr_linear_bf16. */
+int vasr_ssm_block_tail_bf16(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo16,
+                             const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                             const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
+                             int M, int D, int E, void* stream);
+int vasr_pack_weights16_bf16(const uint16_t* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
+int64_t vasr_pack_weights16_bf16_elems(int N, int K);
 /* Split-bf16 planes of a (N, K) fp32 weight in the fragment layout of v_mfma_f32_16x16x32_bf16
  * ([ceil(N/16)][ceil(K/32)][3][64][8] bf16), vasr_split_weights16_elems(N, K) uint16 elements. */
 int vasr_split_weights16_bf16x3(const float* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);

@@ -85,3 +85,23 @@ def test_fused_block_equals_unfused_launches(monkeypatch):
     monkeypatch.setenv("VASR_FUSED_TAIL", "0")
     plain = blk(x)
     torch.testing.assert_close(fused, plain, atol=3e-5, rtol=1e-5)
+
+
+def test_fused_block_bf16_model(monkeypatch):
+    """The bf16 model's fused tail (vasr_ssm_block_tail_bf16: one bf16 plane, activations
+    rounded to bf16 at the MFMA input as vasr_linear_bf16 does) vs the bf16 launches it
+    replaces; both round h and f to bf16, so they agree to bf16 rounding of rare boundary
+    cases."""
+    import velocity_asr as va
+    from velocity_asr import synthetic as S
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    blk = m.to(DEV).eval().to(torch.bfloat16).local_ssm.layers[2]
+    x = torch.from_numpy(np.random.default_rng(6).standard_normal((2, 300, 192)).astype(np.float32)).to(DEV)
+    monkeypatch.setenv("VASR_FUSED_TAIL", "1")
+    fused = blk(x)
+    monkeypatch.setenv("VASR_FUSED_TAIL", "0")
+    plain = blk(x)
+    err = (fused - plain).abs()
+    assert err.max().item() < 2e-2 and err.mean().item() < 1e-3, (err.max().item(), err.mean().item())

@@ -44,8 +44,10 @@ constexpr int TE = 384;          // FFN width = d_inner
 constexpr int TBM = 32;          // token rows per workgroup
 constexpr int TWAVES = 4;
 constexpr int NSTAGES = 36;      // out_proj 12 k-steps, FFN1 2 halves x 6, FFN2 12
-constexpr int PD = 3;            // weight prefetch distance (steps)
-constexpr int RING = PD + 1;
+// weight prefetch distance (steps): 3 for the split planes (9 fragments a step), 6 for one
+// bf16 plane (3 fragments a step)
+template <int NP>
+constexpr int pd_of() { return NP == 3 ? 3 : 6; }
 constexpr int PLANE_E = TBM * TE * 2;  // one bf16 plane of a 384-wide A tile (24 KiB)
 constexpr int PLANE_D = TBM * TD * 2;  // one bf16 plane of a 192-wide A tile (12 KiB)
 
@@ -74,21 +76,24 @@ struct TailParams {
     int M;
 };
 
+template <int NP>
 struct TailCtx {
+    static constexpr int PD = pd_of<NP>();
+    static constexpr int RING = PD + 1;
     const TailParams& P;
     char* R;   // 384-wide planes (g, f) / fp32 x1 scratch
     char* H;   // 192-wide planes (h)
     int lane, wave, r, q, m0;
     floatx4 acc[2][3];
-    bf16x8 w[RING][3][3];  // [ring slot][column tile][plane]
+    bf16x8 w[RING][3][NP];  // [ring slot][column tile][plane]
     float x1[2][3][4];     // residual x, then x1 = out_proj(g) + x
     float bb1[2][3], bb2[3], lnw[3], lnb[3];
 };
 
-// weight fragments of step S for this wave: column tiles 3w .. 3w+2, three planes, from the
-// fragment layout [N/16][K/32][3][64][8]
-template <int S>
-__device__ __forceinline__ void load_w(TailCtx& c) {
+// weight fragments of step S for this wave: column tiles 3w .. 3w+2, NP planes, from the
+// fragment layout [N/16][K/32][NP][64][8]
+template <int S, int NP>
+__device__ __forceinline__ void load_w(TailCtx<NP>& c) {
     const uint16_t* W;
     int nt0, ks, KS;
     if constexpr (S < 12) {
@@ -102,18 +107,32 @@ __device__ __forceinline__ void load_w(TailCtx& c) {
     for (int t = 0; t < 3; ++t) {
         const int nt = nt0 + 3 * c.wave + t;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-            c.w[S % RING][t][pl] =
-                *reinterpret_cast<const bf16x8*>(W + ((int64_t)(nt * KS + ks) * 3 + pl) * 512 + c.lane * 8);
+        for (int pl = 0; pl < NP; ++pl)
+            c.w[S % TailCtx<NP>::RING][t][pl] =
+                *reinterpret_cast<const bf16x8*>(W + ((int64_t)(nt * KS + ks) * NP + pl) * 512 + c.lane * 8);
     }
 }
 
+// the first PD steps' weights (prologue)
+template <int S, int NP>
+__device__ __forceinline__ void load_first(TailCtx<NP>& c) {
+    load_w<S, NP>(c);
+    if constexpr (S + 1 < TailCtx<NP>::PD) load_first<S + 1, NP>(c);
+}
+
+// v as NP bf16 planes: the exact three-way split, or (NP = 1, the bf16 model) v rounded to
+// bf16 as vasr_linear_bf16 rounds its A operand
+template <int NP>
 __device__ __forceinline__ void split_store(char* plane0, int plane_bytes, int off, float v) {
-    __bf16 a, b, cc;
-    gemm::split1(v, a, b, cc);
-    *reinterpret_cast<__bf16*>(plane0 + off) = a;
-    *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = b;
-    *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = cc;
+    if constexpr (NP == 3) {
+        __bf16 a, b, cc;
+        gemm::split1(v, a, b, cc);
+        *reinterpret_cast<__bf16*>(plane0 + off) = a;
+        *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = b;
+        *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = cc;
+    } else {
+        *reinterpret_cast<__bf16*>(plane0 + off) = (__bf16)v;
+    }
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -121,20 +140,21 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
 }
 
-template <int S>
-__device__ __forceinline__ void tail_step(TailCtx& c) {
-    if constexpr (S + PD < NSTAGES) load_w<S + PD>(c);
+template <int S, int NP>
+__device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
+    constexpr int PD = TailCtx<NP>::PD;
+    if constexpr (S + PD < NSTAGES) load_w<S + PD, NP>(c);
     // keep the prefetch where it is: without this fence the scheduler sinks the loads next to
     // their use (to save registers) and the step then waits on them (measured: the weight
     // stream then ran at a third of the L2 rate)
     __builtin_amdgcn_sched_barrier(0);
     // A fragments of both row tiles, three planes each
-    bf16x8 a[2][3];
+    bf16x8 a[2][NP];
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
         const int row = 16 * tm + c.r;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < NP; ++pl) {
             if constexpr (S < 12 || S >= 24) {
                 constexpr int ks = S < 12 ? S : S - 24;
                 a[tm][pl] = *reinterpret_cast<const bf16x8*>(c.R + pl * PLANE_E + row * TE * 2 +
@@ -150,13 +170,15 @@ __device__ __forceinline__ void tail_step(TailCtx& c) {
     for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
         for (int t = 0; t < 3; ++t) {  // small terms first, then the leading hi * hi (as gemm_x3)
-            const bf16x8(&wf)[3] = c.w[S % RING][t];
+            const bf16x8(&wf)[NP] = c.w[S % TailCtx<NP>::RING][t];
             floatx4 v = c.acc[tm][t];
-            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][2], wf[0], v, 0, 0, 0);
-            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[2], v, 0, 0, 0);
-            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[1], v, 0, 0, 0);
-            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[0], v, 0, 0, 0);
-            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[1], v, 0, 0, 0);
+            if constexpr (NP == 3) {
+                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][2], wf[0], v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[2], v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[1], v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[0], v, 0, 0, 0);
+                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[1], v, 0, 0, 0);
+            }
             v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[0], v, 0, 0, 0);
             c.acc[tm][t] = v;
         }
@@ -202,7 +224,7 @@ __device__ __forceinline__ void tail_step(TailCtx& c) {
             const float rstd = 1.0f / sqrtf(var + c.P.ln_eps);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
-                split_store(c.H, PLANE_D, poff<TD>(rr, c.lane + 64 * i), __builtin_fmaf((v[i] - mean) * rstd, c.lnw[i], c.lnb[i]));
+                split_store<NP>(c.H, PLANE_D, poff<TD>(rr, c.lane + 64 * i), __builtin_fmaf((v[i] - mean) * rstd, c.lnw[i], c.lnb[i]));
         }
         lds_barrier();  // h complete; the scratch in R is free for f
     } else if constexpr (S == 17 || S == 23) {
@@ -215,19 +237,20 @@ __device__ __forceinline__ void tail_step(TailCtx& c) {
                 const int col = TD * hh + 16 * (3 * c.wave + t) + c.r;
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    split_store(c.R, PLANE_E, poff<TE>(16 * tm + 4 * c.q + i, col),
+                    split_store<NP>(c.R, PLANE_E, poff<TE>(16 * tm + 4 * c.q + i, col),
                                 gelu_fast(c.acc[tm][t][i] + c.bb1[hh][t]));
                 c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         if constexpr (S == 23) lds_barrier();  // f complete before FFN2 reads it
     }
-    if constexpr (S + 1 < NSTAGES) tail_step<S + 1>(c);
+    if constexpr (S + 1 < NSTAGES) tail_step<S + 1, NP>(c);
 }
 
+template <int NP>
 __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
-    __shared__ __attribute__((aligned(16))) char R[3 * PLANE_E];
-    __shared__ __attribute__((aligned(16))) char H[3 * PLANE_D];
-    TailCtx c{P, R, H};
+    __shared__ __attribute__((aligned(16))) char R[NP * PLANE_E];
+    __shared__ __attribute__((aligned(16))) char H[NP * PLANE_D];
+    TailCtx<NP> c{P, R, H};
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     c.r = c.lane & 15;
@@ -235,9 +258,7 @@ __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
     c.m0 = blockIdx.x * TBM;
     // weights of the first PD steps, then the g tile (split once into R's planes), the residual
     // x and the epilogue constants: all of these loads are in flight together
-    load_w<0>(c);
-    load_w<1>(c);
-    load_w<2>(c);
+    load_first<0, NP>(c);
     __builtin_amdgcn_sched_barrier(0);
     constexpr int UNITS = TBM * TE / 8;  // 8-float chunks of the g tile
 #pragma unroll
@@ -247,12 +268,18 @@ __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
         const float* src = P.g + (int64_t)min(c.m0 + rr, P.M - 1) * P.ldg + 8 * ch;
         const float4 v0 = *reinterpret_cast<const float4*>(src);
         const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
-        bf16x8 hi, mid, lo;
-        split8(v0, v1, hi, mid, lo);
         const int off = rr * TE * 2 + ((ch ^ (rr & 15)) << 4);
-        *reinterpret_cast<bf16x8*>(R + off) = hi;
-        *reinterpret_cast<bf16x8*>(R + PLANE_E + off) = mid;
-        *reinterpret_cast<bf16x8*>(R + 2 * PLANE_E + off) = lo;
+        if constexpr (NP == 3) {
+            bf16x8 hi, mid, lo;
+            split8(v0, v1, hi, mid, lo);
+            *reinterpret_cast<bf16x8*>(R + off) = hi;
+            *reinterpret_cast<bf16x8*>(R + PLANE_E + off) = mid;
+            *reinterpret_cast<bf16x8*>(R + 2 * PLANE_E + off) = lo;
+        } else {
+            const bf16x8 v = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
+                              (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
+            *reinterpret_cast<bf16x8*>(R + off) = v;
+        }
     }
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)
@@ -275,7 +302,7 @@ __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
         c.lnb[i] = P.ln_b[c.lane + 64 * i];
     }
     lds_barrier();  // the g planes are complete
-    tail_step<0>(c);
+    tail_step<0, NP>(c);
     // out = ffn.3(f) + b2 + x1
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)
@@ -318,8 +345,68 @@ __global__ void split_weights16_kernel(const float* __restrict__ W, int64_t ldw,
     *reinterpret_cast<bf16x8*>(out + base + 1024) = lo;
 }
 
+// One bf16 plane (the bf16 model's own weights) in the same layout: [ceil(N/16)][Kp/32][64][8].
+__global__ void pack_weights16_kernel(const uint16_t* __restrict__ W, int64_t ldw, int N, int K, int Kp,
+                                      uint16_t* __restrict__ out) {
+    const int64_t qd = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int cpr = Kp / 8;
+    const int NT = (N + 15) / 16;
+    if (qd >= (int64_t)NT * 16 * cpr) return;
+    const int n = (int)(qd / cpr), k0 = (int)(qd % cpr) * 8;
+    const int KS = Kp / 32;
+    const int ln = 16 * ((k0 % 32) / 8) + n % 16;
+    uint16_t* dst = out + ((int64_t)(n / 16) * KS + k0 / 32) * 512 + ln * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j] = (n < N && k0 + j < K) ? W[(int64_t)n * ldw + k0 + j] : (uint16_t)0;
+}
+
+int tail_args(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo, const float* ln_w,
+              const float* ln_b, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2, float* out,
+              int64_t ldo, int M, int D, int E, const char* fn) {
+    VASR_CHECK_ARG(g && x && wo && ln_w && ln_b && w1 && b1 && w2 && b2 && out, "%s: null pointer", fn);
+    VASR_CHECK_ARG(D == TD && E == TE, "%s: built for d_model %d, FFN width %d (got %d, %d)", fn, TD, TE, D, E);
+    VASR_CHECK_ARG(M >= 0 && ldg >= E && ldx >= D && ldo >= D && ldg % 4 == 0,
+                   "%s: bad shape M=%d ldg=%lld ldx=%lld ldo=%lld", fn, M, (long long)ldg, (long long)ldx,
+                   (long long)ldo);
+    VASR_CHECK_ARG(((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(wo) | reinterpret_cast<uintptr_t>(w1) |
+                     reinterpret_cast<uintptr_t>(w2)) & 15) == 0,
+                   "%s: g and the weight planes must be 16-byte aligned", fn);
+    return VASR_OK;
+}
+
 }  // namespace
 }  // namespace vasr
+
+VASR_API int64_t vasr_pack_weights16_bf16_elems(int N, int K) {
+    if (N <= 0 || K <= 0) return 0;
+    return (int64_t)((N + 15) / 16 * 16) * ((K + 31) / 32 * 32);
+}
+
+VASR_API int vasr_pack_weights16_bf16(const uint16_t* W, int64_t ldw, int N, int K, uint16_t* out, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(W && out, "vasr_pack_weights16_bf16: null pointer");
+    VASR_CHECK_ARG(N > 0 && K > 0 && ldw >= K, "vasr_pack_weights16_bf16: bad shape N=%d K=%d", N, K);
+    VASR_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "vasr_pack_weights16_bf16: out must be 16-B aligned");
+    const int Kp = (K + 31) / 32 * 32;
+    const int64_t n = (int64_t)((N + 15) / 16 * 16) * (Kp / 8);
+    hipLaunchKernelGGL(pack_weights16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), W,
+                       ldw, N, K, Kp, out);
+    return launch_status("vasr_pack_weights16_bf16");
+}
+
+VASR_API int vasr_ssm_block_tail_bf16(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo16,
+                                      const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                                      const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
+                                      int M, int D, int E, void* stream) {
+    using namespace vasr;
+    if (int rc = tail_args(g, ldg, x, ldx, wo16, ln_w, ln_b, w1_16, b1, w2_16, b2, out, ldo, M, D, E,
+                           "vasr_ssm_block_tail_bf16"))
+        return rc;
+    if (M == 0) return VASR_OK;
+    TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
+    hipLaunchKernelGGL(ssm_tail_kernel<1>, dim3((M + TBM - 1) / TBM), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    return launch_status("vasr_ssm_block_tail_bf16");
+}
 
 VASR_API int64_t vasr_split_weights16_elems(int N, int K) {
     if (N <= 0 || K <= 0) return 0;
@@ -343,18 +430,11 @@ VASR_API int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x
                                      const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
                                      int M, int D, int E, void* stream) {
     using namespace vasr;
-    VASR_CHECK_ARG(g && x && wo16 && ln_w && ln_b && w1_16 && b1 && w2_16 && b2 && out,
-                   "vasr_ssm_block_tail_f32: null pointer");
-    VASR_CHECK_ARG(D == TD && E == TE, "vasr_ssm_block_tail_f32: built for d_model %d, FFN width %d (got %d, %d)", TD, TE,
-                   D, E);
-    VASR_CHECK_ARG(M >= 0 && ldg >= E && ldx >= D && ldo >= D && ldg % 4 == 0,
-                   "vasr_ssm_block_tail_f32: bad shape M=%d ldg=%lld ldx=%lld ldo=%lld", M, (long long)ldg,
-                   (long long)ldx, (long long)ldo);
-    VASR_CHECK_ARG(((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(wo16) |
-                     reinterpret_cast<uintptr_t>(w1_16) | reinterpret_cast<uintptr_t>(w2_16)) & 15) == 0,
-                   "vasr_ssm_block_tail_f32: g and the weight planes must be 16-byte aligned");
+    if (int rc = tail_args(g, ldg, x, ldx, wo16, ln_w, ln_b, w1_16, b1, w2_16, b2, out, ldo, M, D, E,
+                           "vasr_ssm_block_tail_f32"))
+        return rc;
     if (M == 0) return VASR_OK;
     TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
-    hipLaunchKernelGGL(ssm_tail_kernel, dim3((M + TBM - 1) / TBM), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(ssm_tail_kernel<3>, dim3((M + TBM - 1) / TBM), dim3(64 * TWAVES), 0, as_stream(stream), p);
     return launch_status("vasr_ssm_block_tail_f32");
 }

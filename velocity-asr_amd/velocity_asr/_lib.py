@@ -65,6 +65,10 @@ _SIGNATURES = {
     "vasr_ssm_scan_workspace_floats": ([ctypes.c_int] * 4, c_i64),
     "vasr_ssm_block_tail_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                 + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
+    "vasr_ssm_block_tail_bf16": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
+                                 + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
+    "vasr_pack_weights16_bf16": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
+    "vasr_pack_weights16_bf16_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_split_weights16_bf16x3": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
     "vasr_split_weights16_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_flac_decode": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p], ctypes.c_int),

@@ -167,13 +167,35 @@ def split_weights16(w: torch.Tensor) -> torch.Tensor:
     return planes
 
 
+def pack_weights16(w: torch.Tensor) -> torch.Tensor:
+    """One bf16 plane of a (N, K) bf16 weight in the v_mfma_f32_16x16x32_bf16 fragment layout
+    (the bf16 model's fused SSMBlock tail), built once per (tensor, version)."""
+    N, K, ldw = _rows("pack16.w", w)
+    sig = (w.data_ptr(), w._version, N, K, ldw)
+    ent = _splits16.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == sig:
+        return ent[2]
+    packed = torch.empty(int(L.lib().vasr_pack_weights16_bf16_elems(N, K)), device=w.device, dtype=torch.int16)
+    check(L.lib().vasr_pack_weights16_bf16(w.data_ptr(), ldw, N, K, packed.data_ptr(), stream_of(w)),
+          "vasr_pack_weights16_bf16")
+    key = id(w)
+    _splits16[key] = (weakref.ref(w, lambda _r, k=key: _splits16.pop(k, None)), sig, packed)
+    return packed
+
+
 def ssm_block_tail(g: torch.Tensor, x: torch.Tensor, wo: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor,
                    ln_eps: float, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Fused SSMBlock tail (vasr_ssm_block_tail_f32): out = ffn(LN2(g Wo^T + x)) + (g Wo^T + x)
-    for g (M, 384) and x (M, 192) row views (d_model 192, FFN width 384)."""
-    for n, t in (("g", g), ("x", x), ("wo", wo), ("ln_w", ln_w), ("ln_b", ln_b), ("w1", w1), ("b1", b1),
-                 ("w2", w2), ("b2", b2)):
+    """Fused SSMBlock tail (vasr_ssm_block_tail_f32, or _bf16 for bf16 weights): out =
+    ffn(LN2(g Wo^T + x)) + (g Wo^T + x) for g (M, 384) and x (M, 192) row views (d_model 192,
+    FFN width 384)."""
+    bf16 = wo.dtype == torch.bfloat16
+    if bf16:
+        if not (w1.dtype == w2.dtype == torch.bfloat16):
+            raise TypeError("ssm_block_tail: mixed weight dtypes")
+        ln_w, ln_b, b1, b2 = f32(ln_w), f32(ln_b), f32(b1), f32(b2)
+    for n, t in (("g", g), ("x", x), ("ln_w", ln_w), ("ln_b", ln_b), ("b1", b1), ("b2", b2)) + (
+            () if bf16 else (("wo", wo), ("w1", w1), ("w2", w2))):
         _cuda_f32(f"ssm_block_tail.{n}", t)
     M, E, ldg = _rows("ssm_block_tail.g", g)
     Mx, D, ldx = _rows("ssm_block_tail.x", x)
@@ -182,12 +204,13 @@ def ssm_block_tail(g: torch.Tensor, x: torch.Tensor, wo: torch.Tensor, ln_w: tor
     if out is None:
         out = torch.empty((M, D), device=g.device, dtype=torch.float32)
     _, _, ldo = _rows("ssm_block_tail.out", out)
+    prep = pack_weights16 if bf16 else split_weights16
+    fn = "vasr_ssm_block_tail_bf16" if bf16 else "vasr_ssm_block_tail_f32"
     ev = _t0("ssm_tail")
-    check(L.lib().vasr_ssm_block_tail_f32(g.data_ptr(), ldg, x.data_ptr(), ldx, split_weights16(wo).data_ptr(),
-                                          ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(), float(ln_eps),
-                                          split_weights16(w1).data_ptr(), b1.contiguous().data_ptr(),
-                                          split_weights16(w2).data_ptr(), b2.contiguous().data_ptr(), out.data_ptr(),
-                                          ldo, M, D, E, stream_of(g)), "vasr_ssm_block_tail_f32")
+    check(getattr(L.lib(), fn)(g.data_ptr(), ldg, x.data_ptr(), ldx, prep(wo).data_ptr(), ln_w.contiguous().data_ptr(),
+                               ln_b.contiguous().data_ptr(), float(ln_eps), prep(w1).data_ptr(),
+                               b1.contiguous().data_ptr(), prep(w2).data_ptr(), b2.contiguous().data_ptr(),
+                               out.data_ptr(), ldo, M, D, E, stream_of(g)), fn)
     _t1("ssm_tail", ev, dict(M=M, D=D, E=E))
     return out
 

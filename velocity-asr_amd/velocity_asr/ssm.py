@@ -125,13 +125,14 @@ class SSMBlock(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def _fused_tail_ok(self, D: int) -> bool:
-        """The one-launch tail (vasr_ssm_block_tail_f32) serves the fp32 model at d_model 192 /
-        FFN width 384 with the split-bf16 GEMM engine; VASR_FUSED_TAIL=0 selects the launches
-        below (read per call so tests can compare the two)."""
+        """The one-launch tail (vasr_ssm_block_tail_f32 / _bf16) serves the fp32 model (split-bf16
+        engine) and the bf16 model at d_model 192 / FFN width 384; VASR_FUSED_TAIL=0 selects the
+        launches below (read per call so tests can compare the two)."""
         w = self.ffn[0].weight
-        return (os.environ.get("VASR_FUSED_TAIL", "1") != "0" and ops.gemm_mode() == "x3"
-                and w.dtype == torch.float32 and D == 192 and tuple(w.shape) == (384, 192)
-                and self.ssm.d_inner == 384)
+        dtype_ok = w.dtype == torch.bfloat16 or (w.dtype == torch.float32 and ops.gemm_mode() == "x3")
+        return (os.environ.get("VASR_FUSED_TAIL", "1") != "0" and dtype_ok and D == 192
+                and tuple(w.shape) == (384, 192) and self.ssm.d_inner == 384
+                and self.ssm.out_proj.weight.dtype == w.dtype == self.ffn[3].weight.dtype)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _check_eval(self)
