@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 8
+#define VASR_ABI_VERSION 9
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -201,6 +201,19 @@ int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x, int64_t
                             const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
                             const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
                             int M, int D, int E, void* stream);
+/* The head of SSMBlock._forward_impl + SelectiveSSM's projections (ssm.py:404-414, :105-113)
+ * in one launch for d_model D = 192, d_inner Di = 384, Nx = 2N + Di = 512 (N = 64):
+ *   u = causal_dwconv4(LayerNorm(x; ln_w, ln_b, ln_eps); conv_w (D, 4), conv_b), per utterance
+ *       of L tokens (M = B * L rows);
+ *   xz = u @ Win^T -> (M, 2 Di) [x_p | z];  xdt = x_p @ Wxd^T + bxd, softplus on columns >= n_sp
+ *       -> (M, Nx) [B | C | dt]
+ * Win / Wxd as vasr_split_weights16_bf16x3 planes (bf16 = 0) or vasr_pack_weights16_bf16 planes
+ * of bf16 weights (bf16 = 1: the bf16 model's arithmetic).  u never leaves the chip. */
+int vasr_ssm_block_head_f32(const float* x, int64_t ldx, const float* ln_w, const float* ln_b, float ln_eps,
+                            const float* conv_w, const float* conv_b, const uint16_t* win16,
+                            const uint16_t* wxd16, const float* bxd, int n_sp, float* xz, int64_t ldxz,
+                            float* xdt, int64_t ldxdt, int M, int L, int D, int Di, int Nx, int bf16,
+                            void* stream);
 /* The same tail for the bf16 model (C3): weights as one bf16 plane (vasr_pack_weights16_bf16 of
  * the bf16 parameters), activations rounded to bf16 at the MFMA input, fp32 accumulation and
  * fp32 LayerNorm / bias / GELU / residual -- the arithmetic of vasr_linear_bf16. */

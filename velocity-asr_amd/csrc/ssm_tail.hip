@@ -29,34 +29,22 @@
 // of row r at c ^ (r & 15) (384-wide) or c ^ (r & 7) (192-wide): conflict-free fragment reads.
 // LDS: 72 KiB for the 384-wide planes (g, then f; the fp32 x1 scratch of the LayerNorm lives
 // there in between) + 36 KiB for the 192-wide planes of h.
-#include "gemm_split.h"
+#include "ssm_fused.h"
 
 namespace vasr {
 namespace {
 
-using gemm::bf16x8;
+using namespace fused;
 using gemm::split8;
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int TD = 192;          // d_model
-constexpr int TE = 384;          // FFN width = d_inner
-constexpr int TBM = 32;          // token rows per workgroup
-constexpr int TWAVES = 4;
 constexpr int NSTAGES = 36;      // out_proj 12 k-steps, FFN1 2 halves x 6, FFN2 12
 // weight prefetch distance (steps): 3 for the split planes (9 fragments a step), 6 for one
-// bf16 plane (3 fragments a step)
+// bf16 plane (3 fragments a step); 2, 4 and 5 measured within 1 us of 3 (tools/tailpd_ab.sh)
+#ifndef VASR_TAIL_PD
+#define VASR_TAIL_PD 3
+#endif
 template <int NP>
-constexpr int pd_of() { return NP == 3 ? 3 : 6; }
-constexpr int PLANE_E = TBM * TE * 2;  // one bf16 plane of a 384-wide A tile (24 KiB)
-constexpr int PLANE_D = TBM * TD * 2;  // one bf16 plane of a 192-wide A tile (12 KiB)
-
-// byte offset of bf16 element (r, col) in one plane: 8-element (16-B) chunks, swizzled
-template <int WIDTH>
-__device__ __forceinline__ int poff(int r, int col) {
-    constexpr int SW = WIDTH == TE ? 15 : 7;
-    return r * WIDTH * 2 + ((((col >> 3) ^ (r & SW))) << 4) + ((col & 7) << 1);
-}
+constexpr int pd_of() { return NP == 3 ? VASR_TAIL_PD : 6; }
 
 struct TailParams {
     const float* g;
@@ -120,26 +108,6 @@ __device__ __forceinline__ void load_first(TailCtx<NP>& c) {
     if constexpr (S + 1 < TailCtx<NP>::PD) load_first<S + 1, NP>(c);
 }
 
-// v as NP bf16 planes: the exact three-way split, or (NP = 1, the bf16 model) v rounded to
-// bf16 as vasr_linear_bf16 rounds its A operand
-template <int NP>
-__device__ __forceinline__ void split_store(char* plane0, int plane_bytes, int off, float v) {
-    if constexpr (NP == 3) {
-        __bf16 a, b, cc;
-        gemm::split1(v, a, b, cc);
-        *reinterpret_cast<__bf16*>(plane0 + off) = a;
-        *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = b;
-        *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = cc;
-    } else {
-        *reinterpret_cast<__bf16*>(plane0 + off) = (__bf16)v;
-    }
-}
-
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (prefetch stays in flight)
-    __builtin_amdgcn_s_barrier();
-}
-
 template <int S, int NP>
 __device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
     constexpr int PD = TailCtx<NP>::PD;
@@ -148,40 +116,19 @@ __device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
     // their use (to save registers) and the step then waits on them (measured: the weight
     // stream then ran at a third of the L2 rate)
     __builtin_amdgcn_sched_barrier(0);
-    // A fragments of both row tiles, three planes each
+    // A fragments of both row tiles
     bf16x8 a[2][NP];
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
-        const int row = 16 * tm + c.r;
-#pragma unroll
-        for (int pl = 0; pl < NP; ++pl) {
-            if constexpr (S < 12 || S >= 24) {
-                constexpr int ks = S < 12 ? S : S - 24;
-                a[tm][pl] = *reinterpret_cast<const bf16x8*>(c.R + pl * PLANE_E + row * TE * 2 +
-                                                             (((4 * ks + c.q) ^ (row & 15)) << 4));
-            } else {
-                constexpr int ks = (S - 12) % 6;
-                a[tm][pl] = *reinterpret_cast<const bf16x8*>(c.H + pl * PLANE_D + row * TD * 2 +
-                                                             (((4 * ks + c.q) ^ (row & 7)) << 4));
-            }
-        }
+        if constexpr (S < 12 || S >= 24)
+            read_a<NP, TE>(c.R, 16 * tm + c.r, S < 12 ? S : S - 24, c.q, a[tm]);
+        else
+            read_a<NP, TD>(c.H, 16 * tm + c.r, (S - 12) % 6, c.q, a[tm]);
     }
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {  // small terms first, then the leading hi * hi (as gemm_x3)
-            const bf16x8(&wf)[NP] = c.w[S % TailCtx<NP>::RING][t];
-            floatx4 v = c.acc[tm][t];
-            if constexpr (NP == 3) {
-                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][2], wf[0], v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[2], v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[1], v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][1], wf[0], v, 0, 0, 0);
-                v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[1], v, 0, 0, 0);
-            }
-            v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tm][0], wf[0], v, 0, 0, 0);
-            c.acc[tm][t] = v;
-        }
+        for (int t = 0; t < 3; ++t) c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % TailCtx<NP>::RING][t], c.acc[tm][t]);
 
     if constexpr (S == 11) {
         // x1 = out_proj(g) + x (registers, kept for the final residual) -> fp32 scratch in R
@@ -268,18 +215,7 @@ __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
         const float* src = P.g + (int64_t)min(c.m0 + rr, P.M - 1) * P.ldg + 8 * ch;
         const float4 v0 = *reinterpret_cast<const float4*>(src);
         const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
-        const int off = rr * TE * 2 + ((ch ^ (rr & 15)) << 4);
-        if constexpr (NP == 3) {
-            bf16x8 hi, mid, lo;
-            split8(v0, v1, hi, mid, lo);
-            *reinterpret_cast<bf16x8*>(R + off) = hi;
-            *reinterpret_cast<bf16x8*>(R + PLANE_E + off) = mid;
-            *reinterpret_cast<bf16x8*>(R + 2 * PLANE_E + off) = lo;
-        } else {
-            const bf16x8 v = {(__bf16)v0.x, (__bf16)v0.y, (__bf16)v0.z, (__bf16)v0.w,
-                              (__bf16)v1.x, (__bf16)v1.y, (__bf16)v1.z, (__bf16)v1.w};
-            *reinterpret_cast<bf16x8*>(R + off) = v;
-        }
+        split_store8<NP>(R, PLANE_E, rr * TE * 2 + ((ch ^ (rr & 15)) << 4), v0, v1);
     }
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)

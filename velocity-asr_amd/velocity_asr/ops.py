@@ -215,6 +215,34 @@ def ssm_block_tail(g: torch.Tensor, x: torch.Tensor, wo: torch.Tensor, ln_w: tor
     return out
 
 
+def ssm_block_head(x: torch.Tensor, B: int, Lq: int, ln_w, ln_b, ln_eps: float, conv_w, conv_b, w_in: torch.Tensor,
+                   w_xdt: torch.Tensor, b_xdt: torch.Tensor, n_sp: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused SSMBlock head (vasr_ssm_block_head_f32): LN1 + causal dwconv -> in_proj -> [x_proj;
+    dt_proj] (+bias, softplus from column n_sp).  x (B*L, 192) -> (xz (B*L, 768), xdt (B*L, 512))."""
+    bf16 = w_in.dtype == torch.bfloat16
+    ln_w, ln_b, conv_w, conv_b, b_xdt = f32(ln_w), f32(ln_b), f32(conv_w), f32(conv_b), f32(b_xdt)
+    for n, t in (("x", x), ("ln_w", ln_w), ("ln_b", ln_b), ("conv_w", conv_w), ("conv_b", conv_b), ("b_xdt", b_xdt)):
+        _cuda_f32(f"ssm_block_head.{n}", t)
+    if bf16 != (w_xdt.dtype == torch.bfloat16):
+        raise TypeError("ssm_block_head: mixed weight dtypes")
+    M, D, ldx = _rows("ssm_block_head.x", x)
+    E2, Dw = w_in.shape
+    Nx, Di = w_xdt.shape
+    if M != B * Lq or Dw != D or E2 != 2 * Di or b_xdt.numel() != Nx:
+        raise ValueError("ssm_block_head: inconsistent shapes")
+    prep = pack_weights16 if bf16 else split_weights16
+    xz = torch.empty((M, E2), device=x.device, dtype=torch.float32)
+    xdt = torch.empty((M, Nx), device=x.device, dtype=torch.float32)
+    ev = _t0("ssm_head")
+    check(L.lib().vasr_ssm_block_head_f32(x.data_ptr(), ldx, ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(),
+                                          float(ln_eps), conv_w.contiguous().data_ptr(), conv_b.contiguous().data_ptr(),
+                                          prep(w_in).data_ptr(), prep(w_xdt).data_ptr(), b_xdt.contiguous().data_ptr(),
+                                          int(n_sp), xz.data_ptr(), E2, xdt.data_ptr(), Nx, M, Lq, D, Di, Nx, int(bf16),
+                                          stream_of(x)), "vasr_ssm_block_head_f32")
+    _t1("ssm_head", ev, dict(M=M, D=D, Di=Di, Nx=Nx))
+    return xz, xdt
+
+
 def pack_bf16(w: torch.Tensor) -> torch.Tensor:
     """One fragment-native bf16 plane (as int16 storage) of a (N, K) bf16 weight view."""
     N, K, ldw = _rows("pack.w", w)

@@ -93,6 +93,12 @@ class SelectiveSSM(nn.Module):
         xz = ops.gemm(u, self.in_proj.weight)                                   # (M, 2Di) [x | z]
         xdt = ops.gemm(xz[:, :Di], p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM,
                        n_out=2 * N)                                              # (M, 2N + Di) [B | C | dt]
+        return self.scan(xz, xdt, B, L)
+
+    def scan(self, xz: torch.Tensor, xdt: torch.Tensor, B: int, L: int) -> torch.Tensor:
+        """The gated scan over in_proj's [x | z] and [B | C | dt]."""
+        p = self._prepared()
+        N = self.state_dim
         mode = _SCAN_MODE_ID[self.scan_mode]
         return ops.ssm_scan(xz, xdt[:, 2 * N:], xdt[:, :2 * N], p["A2"], self.D, B, L,
                             _tree_mode() if mode == 0 else mode)
@@ -134,14 +140,34 @@ class SSMBlock(nn.Module):
                 and tuple(w.shape) == (384, 192) and self.ssm.d_inner == 384
                 and self.ssm.out_proj.weight.dtype == w.dtype == self.ffn[3].weight.dtype)
 
+    def _fused_head_ok(self, D: int) -> bool:
+        """The one-launch head (vasr_ssm_block_head_f32: d_model 192, d_inner 384, state dim 64,
+        kernel 4) is opt-in (VASR_FUSED_HEAD=1): alone it matches the three launches (59.6 vs
+        62.2 us per 16-clip block) but end to end it is slower (119k vs 132k RTFx: one 108-KB-LDS
+        block per CU for its whole duration keeps the other stream's scan off those CUs), and at
+        B = 1 its 2 MB weight stream per 32-row block makes it slower alone too (49 vs 38 us)."""
+        w = self.ssm.in_proj.weight
+        dtype_ok = w.dtype == torch.bfloat16 or (w.dtype == torch.float32 and ops.gemm_mode() == "x3")
+        return (os.environ.get("VASR_FUSED_HEAD", "0") == "1" and dtype_ok and D == 192
+                and self.ssm.d_inner == 384 and self.ssm.state_dim == 64 and self.conv.kernel_size[0] == 4
+                and self.ssm.x_proj.weight.dtype == self.ssm.dt_proj.weight.dtype == w.dtype)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _check_eval(self)
         B, L, D = x.shape
         x = x.contiguous()
-        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
-                          self.conv.bias, self.norm1.eps)
-        g = self.ssm.gated_scan(u.view(B * L, D), B, L)
         x2 = x.view(B * L, D)
+        if self._fused_head_ok(D):
+            # LN1 + causal dwconv -> in_proj -> [x_proj; dt_proj] + softplus in one kernel (u stays on chip)
+            p = self.ssm._prepared()
+            xz, xdt = ops.ssm_block_head(x2, B, L, self.norm1.weight, self.norm1.bias, self.norm1.eps,
+                                         ops.f32(self.conv.weight).view(D, -1), self.conv.bias,
+                                         self.ssm.in_proj.weight, p["w_xdt"], p["b_xdt"], 2 * self.ssm.state_dim)
+            g = self.ssm.scan(xz, xdt, B, L)
+        else:
+            u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
+                              self.conv.bias, self.norm1.eps)
+            g = self.ssm.gated_scan(u.view(B * L, D), B, L)
         if self._fused_tail_ok(D):
             # out_proj + residual -> LN2 -> FFN1 + GELU -> FFN2 + residual in one kernel:
             # x1 and the FFN intermediate stay on chip
