@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 9
+#define VASR_ABI_VERSION 10
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -41,6 +41,13 @@ extern "C" {
 /* ABI version (== VASR_ABI_VERSION) and last-error text. */
 int vasr_version(void);
 const char* vasr_last_error(void);
+
+/* Runtime helpers: a HIP stream restricted to the CUs set in `mask` (hipExtStreamCreateWithCUMask;
+ * bit i = logical CU i) for running independent utterance groups on disjoint parts of the chip,
+ * its destruction, and the device's CU count. */
+int vasr_stream_create_cu_mask(const uint32_t* mask, int words, void** stream_out);
+int vasr_stream_destroy(void* stream);
+int vasr_device_cu_count(void);
 
 /* ------------------------------------------------------------------ GEMM
  * C[b] = epilogue(A[b] (M x K) * W^T (K x N) + bias), W row-major [N][K] as in

@@ -43,6 +43,40 @@ def token_lists(toks: torch.Tensor, lens: torch.Tensor) -> List[List[int]]:
     return [t[b, : n[b]].tolist() for b in range(t.shape[0])]
 
 
+def _cu_masks(n_streams: int, mode: str, n_cu: int):
+    """Per-stream CU masks (lists of uint32 words): "half" = contiguous blocks of logical CU ids,
+    "interleave" = CU i to stream i % n_streams."""
+    words = (n_cu + 31) // 32
+    masks = []
+    for s in range(n_streams):
+        m = [0] * words
+        for cu in range(n_cu):
+            own = (cu * n_streams // n_cu == s) if mode == "half" else (cu % n_streams == s)
+            if own:
+                m[cu // 32] |= 1 << (cu % 32)
+        masks.append(m)
+    return masks
+
+
+class _MaskedStream:
+    """A torch ExternalStream over a CU-masked HIP stream created (and destroyed) by the library."""
+
+    def __init__(self, device: torch.device, mask):
+        import ctypes
+        arr = (ctypes.c_uint32 * len(mask))(*mask)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            ops.check(ops.L.lib().vasr_stream_create_cu_mask(arr, len(mask), ctypes.byref(h)),
+                      "vasr_stream_create_cu_mask")
+        self.handle = h.value
+        self.stream = torch.cuda.ExternalStream(self.handle, device=device)
+
+    def close(self):
+        if self.handle is not None:
+            ops.L.lib().vasr_stream_destroy(self.handle)
+            self.handle = None
+
+
 def _model_fingerprint(model: torch.nn.Module):
     """(tensor, data_ptr, version) of every parameter and buffer: a captured graph holds raw
     pointers to them and to the derived weight layouts built from them (split-bf16 planes,
@@ -70,7 +104,7 @@ class GraphedTranscriber:
     """
 
     def __init__(self, model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
-                 warmup: int = 2, streams: int = 1):
+                 warmup: int = 2, streams: int = 1, cu_split: Optional[str] = None):
         self.model = model
         dev = device or next(model.parameters()).device
         self.device = dev
@@ -82,7 +116,20 @@ class GraphedTranscriber:
         self.tokens = torch.zeros((batch, L), device=dev, dtype=torch.int32)
         self.lengths = torch.zeros((batch,), device=dev, dtype=torch.int32)
         g = batch // streams
-        self.streams = [torch.cuda.Stream(dev) for _ in range(streams)]
+        # cu_split ("half" | "interleave"; VASR_CU_SPLIT): each utterance group's stream owns a
+        # disjoint share of the CUs (hipExtStreamCreateWithCUMask) instead of competing for all.
+        # Measured much slower (65k / 91k vs 133k RTFx, tools/ab_env.sh): the groups' kernels
+        # are latency-bound and gain from every CU; kept as an option, off by default.
+        cu_split = cu_split if cu_split is not None else os.environ.get("VASR_CU_SPLIT", "none")
+        self._masked = []
+        if streams > 1 and cu_split in ("half", "interleave"):
+            n_cu = int(ops.L.lib().vasr_device_cu_count())
+            self._masked = [_MaskedStream(dev, m) for m in _cu_masks(streams, cu_split, n_cu)]
+            self.streams = [m.stream for m in self._masked]
+        elif cu_split not in ("none", "", None):
+            raise ValueError(f"cu_split {cu_split!r}: expected none, half or interleave")
+        else:
+            self.streams = [torch.cuda.Stream(dev) for _ in range(streams)]
         views = [self.audio[i * g:(i + 1) * g] for i in range(streams)]
         outs = [(self.tokens[i * g:(i + 1) * g], self.lengths[i * g:(i + 1) * g]) for i in range(streams)]
         main = torch.cuda.current_stream(dev)
