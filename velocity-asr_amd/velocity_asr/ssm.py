@@ -82,14 +82,34 @@ class SelectiveSSM(nn.Module):
             # pre-scaled by log2(e) so the kernel's dA is one v_exp_f32.
             A = -torch.exp(self.A_log.detach().float().cpu())
             A2 = (A * torch.tensor(ops.LOG2E, dtype=torch.float32)).to(dev)
-            return dict(w_xdt=w, b_xdt=b, A2=A2)
-        return cached(self, "ssm", (self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, self.A_log),
-                      build)
+            out = dict(w_xdt=w, b_xdt=b, A2=A2)
+            if w.dtype == torch.float32:
+                # composed projection: [x_proj; dt_proj](in_proj_x(u)) = u @ (W_xdt W_in_x)^T, the
+                # product formed in float64 and rounded once (see gated_scan)
+                Di = self.d_inner
+                wc = (w.detach().double() @ self.in_proj.weight.detach()[:Di].double()).float()
+                out["w_comb"] = torch.cat([self.in_proj.weight.detach(), wc], 0).contiguous()
+                out["b_comb"] = torch.cat([torch.zeros(2 * Di, device=dev), b]).contiguous()
+            return out
+        return cached(self, "ssm", (self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, self.A_log,
+                                    self.in_proj.weight), build)
 
     def gated_scan(self, u: torch.Tensor, B: int, L: int) -> torch.Tensor:
-        """u (B*L, d_model) -> y * silu(z) of shape (B*L, d_inner), before out_proj."""
+        """u (B*L, d_model) -> y * silu(z) of shape (B*L, d_inner), before out_proj.
+
+        fp32 model (default): in_proj and [x_proj; dt_proj] as ONE GEMM of u against
+        [W_in; W_xdt W_in_x] (N = 2 Di + 2N + Di, K = d_model), softplus on the dt columns: the
+        composition of two linear maps, with the composed matrix formed in float64 and rounded
+        once.  It skips the fp32 rounding of x_p between the two products (a ~1e-7 relative
+        difference, the size of GEMM accumulation-order effects) and needs 29 % fewer MACs, one
+        launch instead of two and no re-read of x_p.  VASR_XDT_COMPOSE=0 selects the two
+        products as the reference evaluates them (ssm.py:105-113)."""
         p = self._prepared()
         Di, N = self.d_inner, self.state_dim
+        if "w_comb" in p and os.environ.get("VASR_XDT_COMPOSE", "1") != "0":
+            out = ops.gemm(u, p["w_comb"], p["b_comb"], epilogue=_lib.EPI_SOFTPLUS_FROM,
+                           n_out=2 * Di + 2 * N)                                 # (M, 2Di + 2N + Di)
+            return self.scan(out[:, :2 * Di], out[:, 2 * Di:], B, L)
         xz = ops.gemm(u, self.in_proj.weight)                                   # (M, 2Di) [x | z]
         xdt = ops.gemm(xz[:, :Di], p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM,
                        n_out=2 * N)                                              # (M, 2N + Di) [B | C | dt]
