@@ -3,8 +3,8 @@ in_proj -> [x_proj; dt_proj] + softplus in one kernel (reference ssm.py:404-414,
 
 Compared with the three launches it replaces (fp32 split-bf16 products: equal to fp32
 accumulation-order rounding), including row tiles that straddle utterance boundaries (the
-conv's causal window must not reach into the previous utterance), and at model level by the
-golden-pinned parity suite, which runs with the fused head (the default)."""
+conv's causal window must not reach into the previous utterance).  The head is opt-in
+(VASR_FUSED_HEAD=1; measured slower end to end)."""
 
 import numpy as np
 import pytest
