@@ -257,6 +257,54 @@ def sequential_scan(x, dt, A, Bm, Cm, D):
     return (y + x * D).astype(f32)
 
 
+def selective_scan_ref(u, delta, A, Bv, Cv, D=None, z=None, delta_bias=None, delta_softplus=False):
+    """Restatement of mamba_ssm's published reference algorithm, ``selective_scan_ref``
+    (state-spaces/mamba, ``mamba_ssm/ops/selective_scan_interface.py``; the function its CUDA
+    ``selective_scan_fn`` is tested against).  mamba-ssm is absent here and unpinned by the
+    reference (not in ``requirements.txt``); the algorithm is the same in every 1.x/2.x release:
+    u, delta (B, D, L); A (D, N); variable Bv, Cv (B, G, N, L) with D % G == 0;
+    deltaA = exp(delta A), deltaB_u = delta B u, x_t = deltaA_t x_{t-1} + deltaB_u_t,
+    y_t = <x_t, C_t>, out = y + u D, then out * silu(z) if z is given."""
+    u = u.astype(f32)
+    delta = delta.astype(f32)
+    if delta_bias is not None:
+        delta = (delta + delta_bias[None, :, None]).astype(f32)
+    if delta_softplus:
+        delta = softplus(delta)
+    Bsz, Dd, L = u.shape
+    N = A.shape[1]
+    G = Bv.shape[1]
+    Bx = np.repeat(Bv, Dd // G, axis=1).astype(f32)  # (B, D, N, L), "b g n l -> b (g h) n l"
+    Cx = np.repeat(Cv, Dd // G, axis=1).astype(f32)
+    deltaA = np.exp(delta[:, :, :, None] * A[None, :, None, :]).astype(f32)           # b d l n
+    deltaB_u = (delta[:, :, :, None] * Bx.transpose(0, 1, 3, 2) * u[:, :, :, None]).astype(f32)
+    x = np.zeros((Bsz, Dd, N), f32)
+    ys = np.empty((Bsz, Dd, L), f32)
+    for i in range(L):
+        x = (deltaA[:, :, i] * x + deltaB_u[:, :, i]).astype(f32)
+        ys[:, :, i] = np.einsum("bdn,bdn->bd", x, Cx[:, :, :, i]).astype(f32)
+    out = ys if D is None else (ys + u * D[None, :, None]).astype(f32)
+    if z is not None:
+        out = (out * silu(z.astype(f32))).astype(f32)
+    return out
+
+
+def mamba_scan(x, dt, A, Bm, Cm, D):
+    """_mamba_scan (ssm.py:297-337) in the layout selective_scan_fn documents: u = x^T,
+    delta = dt^T (B, D, L), A expanded to (D, N), B and C as (B, 1, N, L) with no delta bias
+    or softplus (applied before, ssm.py:113), z = None; the result transposed back to
+    (B, L, D).  The reference itself passes B and C as (B, 1, L, N) (ssm.py:318-321), which
+    the package's shape check rejects unless L == N: this restates the call as
+    the package defines it."""
+    Di = x.shape[2]
+    u = x.transpose(0, 2, 1)
+    delta = dt.transpose(0, 2, 1)
+    Ad = np.broadcast_to(A[None, :], (Di, A.shape[0]))
+    Bv = Bm.transpose(0, 2, 1)[:, None]
+    Cv = Cm.transpose(0, 2, 1)[:, None]
+    return selective_scan_ref(u, delta, Ad, Bv, Cv, D).transpose(0, 2, 1)
+
+
 def discretize(x, dt, A, Bm):
     """_parallel_scan discretisation (ssm.py:196-202): dA = exp(dt*A), x_dB = x*(dt*B)."""
     dA = np.exp(dt[..., None] * A).astype(f32)

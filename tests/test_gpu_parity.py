@@ -244,6 +244,17 @@ def test_scan_lane_layouts(va, monkeypatch, npl, N, L, mode):
     np.testing.assert_allclose(got, ref, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("L", [1, 17, 501])
+def test_mamba_mode_vs_selective_scan_ref(va, L):
+    """scan_mode="mamba" runs the recurrence kernel (mode 1); checked against the oracle's
+    restatement of mamba-ssm's selective_scan_ref in the package's documented layout (the
+    package is absent: parity with it is unpinned)."""
+    x, dt, Bm, Cm, A_log, D = _scan_inputs(300 + L, 2, L, 32, 64)
+    A = (-np.exp(A_log)).astype(np.float32)
+    np.testing.assert_allclose(_run_scan(x, dt, Bm, Cm, A_log, D, 1), R.mamba_scan(x, dt, A, Bm, Cm, D),
+                               atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("N", [16, 32, 64])
 def test_scan_state_dims(va, N):
     x, dt, Bm, Cm, A_log, D = _scan_inputs(77 + N, 2, 70, 64, N)

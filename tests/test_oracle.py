@@ -78,6 +78,47 @@ def test_scan_matches_reference(case):
         assert np.abs(g[name + "__parallel"] - g[name + "__sequential"]).max() > 1e-2
 
 
+@pytest.mark.parametrize("case", _scan_cases(), ids=lambda c: c[0])
+def test_mamba_restatement_is_the_sequential_golden(case):
+    """scan_mode="mamba" (ssm.py:297-337) calls mamba-ssm's selective_scan_fn, absent here
+    (parity unpinned against the package itself): its published reference algorithm,
+    restated in the oracle with the documented (B, G, N, L) layout, is the recurrence whose
+    reference outputs are the `__sequential` goldens."""
+    name, seed, B, L, Di, N = case
+    g = golden("scan.npz")
+    x, dt, Bm, Cm, A_log, D = scan_inputs(seed, B, L, Di, N)
+    A = (-np.exp(A_log)).astype(np.float32)
+    ym = R.mamba_scan(x, dt, A, Bm, Cm, D)
+    np.testing.assert_allclose(ym, g[name + "__sequential"], atol=5e-5, rtol=5e-5)
+
+
+def test_selective_scan_ref_groups_gate_bias():
+    """selective_scan_ref restatement beyond the reference's call: B/C groups, the z gate,
+    delta bias + softplus, against a direct per-channel loop."""
+    rng = np.random.default_rng(7)
+    Bsz, Dd, L, N, G = 2, 8, 13, 4, 2
+    u = rng.standard_normal((Bsz, Dd, L)).astype(np.float32)
+    delta = rng.standard_normal((Bsz, Dd, L)).astype(np.float32)
+    A = -np.exp(rng.standard_normal((Dd, N))).astype(np.float32)
+    Bv = rng.standard_normal((Bsz, G, N, L)).astype(np.float32)
+    Cv = rng.standard_normal((Bsz, G, N, L)).astype(np.float32)
+    D = rng.standard_normal(Dd).astype(np.float32)
+    z = rng.standard_normal((Bsz, Dd, L)).astype(np.float32)
+    bias = rng.standard_normal(Dd).astype(np.float32)
+    got = R.selective_scan_ref(u, delta, A, Bv, Cv, D, z=z, delta_bias=bias, delta_softplus=True)
+    dl = np.log1p(np.exp((delta + bias[None, :, None]).astype(np.float64)))
+    want = np.zeros((Bsz, Dd, L))
+    for b in range(Bsz):
+        for d in range(Dd):
+            gi = d // (Dd // G)
+            h = np.zeros(N)
+            for t in range(L):
+                h = np.exp(dl[b, d, t] * A[d]) * h + dl[b, d, t] * Bv[b, gi, :, t] * u[b, d, t]
+                want[b, d, t] = h @ Cv[b, gi, :, t] + u[b, d, t] * D[d]
+    want *= z / (1.0 + np.exp(-z.astype(np.float64)))
+    np.testing.assert_allclose(got, want, atol=1e-4, rtol=1e-4)
+
+
 def scan_inputs(seed, B, L, Di, N):
     """Same draws as tests/golden/gen_goldens.py:scan_inputs."""
     rng = np.random.default_rng(seed)
