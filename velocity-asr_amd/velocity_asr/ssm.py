@@ -95,7 +95,13 @@ class SelectiveSSM(nn.Module):
                                     self.in_proj.weight), build)
 
     def gated_scan(self, u: torch.Tensor, B: int, L: int) -> torch.Tensor:
-        """u (B*L, d_model) -> y * silu(z) of shape (B*L, d_inner), before out_proj.
+        """u (B*L, d_model) -> y * silu(z) of shape (B*L, d_inner), before out_proj."""
+        xz, xdt = self.project(u)
+        return self.scan(xz, xdt, B, L)
+
+    def project(self, u: torch.Tensor):
+        """u (B*L, d_model) -> (xz, xdt): the scan's operands, [x_p | z] and [B | C | dt]
+        (views into one buffer for the composed projection).
 
         fp32 model (default): in_proj and [x_proj; dt_proj] as ONE GEMM of u against
         [W_in; W_xdt W_in_x] (N = 2 Di + 2N + Di, K = d_model), softplus on the dt columns: the
@@ -109,11 +115,11 @@ class SelectiveSSM(nn.Module):
         if "w_comb" in p and os.environ.get("VASR_XDT_COMPOSE", "1") != "0":
             out = ops.gemm(u, p["w_comb"], p["b_comb"], epilogue=_lib.EPI_SOFTPLUS_FROM,
                            n_out=2 * Di + 2 * N)                                 # (M, 2Di + 2N + Di)
-            return self.scan(out[:, :2 * Di], out[:, 2 * Di:], B, L)
+            return out[:, :2 * Di], out[:, 2 * Di:]
         xz = ops.gemm(u, self.in_proj.weight)                                   # (M, 2Di) [x | z]
         xdt = ops.gemm(xz[:, :Di], p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM,
                        n_out=2 * N)                                              # (M, 2N + Di) [B | C | dt]
-        return self.scan(xz, xdt, B, L)
+        return xz, xdt
 
     def scan(self, xz: torch.Tensor, xdt: torch.Tensor, B: int, L: int) -> torch.Tensor:
         """The gated scan over in_proj's [x | z] and [B | C | dt]."""
@@ -175,6 +181,18 @@ class SSMBlock(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _check_eval(self)
         B, L, D = x.shape
+        x2, xz, xdt = self.head(x)
+        g = self.ssm.scan(xz, xdt, B, L)
+        return self.tail(g, x2, B, L)
+
+    # The block in three stages -- head (LN1, causal dwconv, projections), the scan, tail (out_proj
+    # + residual, LN2, FFN + residual).  (Issuing one utterance group's scans on a stream of their
+    # own beside the other group's heads and tails measured slower than independent group
+    # streams: profiles/r02_paired/.)
+    def head(self, x: torch.Tensor):
+        """x (B, L, D) -> (x2 = x as (B*L, D) rows, xz, xdt): the scan's operands."""
+        _check_eval(self)
+        B, L, D = x.shape
         x = x.contiguous()
         x2 = x.view(B * L, D)
         if self._fused_head_ok(D):
@@ -183,11 +201,15 @@ class SSMBlock(nn.Module):
             xz, xdt = ops.ssm_block_head(x2, B, L, self.norm1.weight, self.norm1.bias, self.norm1.eps,
                                          ops.f32(self.conv.weight).view(D, -1), self.conv.bias,
                                          self.ssm.in_proj.weight, p["w_xdt"], p["b_xdt"], 2 * self.ssm.state_dim)
-            g = self.ssm.scan(xz, xdt, B, L)
         else:
             u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
                               self.conv.bias, self.norm1.eps)
-            g = self.ssm.gated_scan(u.view(B * L, D), B, L)
+            xz, xdt = self.ssm.project(u.view(B * L, D))
+        return x2, xz, xdt
+
+    def tail(self, g: torch.Tensor, x2: torch.Tensor, B: int, L: int) -> torch.Tensor:
+        """Gated scan output g (B*L, d_inner) and the block input rows x2 -> block output (B, L, D)."""
+        D = x2.shape[1]
         if self._fused_tail_ok(D):
             # out_proj + residual -> LN2 -> FFN1 + GELU -> FFN2 + residual in one kernel:
             # x1 and the FFN intermediate stay on chip
