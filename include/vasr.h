@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 10
+#define VASR_ABI_VERSION 11
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -266,6 +266,17 @@ int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t stride_p
                           const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
                           float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
                           int normalize, float* workspace, void* stream);
+/* Utterances of different lengths in one zero-padded batch (the _var entry points below and
+ * vasr_stft_power_400_var_f32, vasr_adaptive_pool_var_f32, vasr_pooled_attention_var_f32,
+ * vasr_ctc_collapse_var): a device int32 array gives each utterance's own size, and every
+ * value an utterance keeps is the one it gets alone (the reference runs one file at a time,
+ * scripts/evaluate.py:91-98).  Here frames[b] <= F is utterance b's frame count: its
+ * statistics cover its own frames only and its later frames are written as 0.  Needs
+ * ld_power <= 256 and n_mels <= 85 (the chunked pass). */
+int vasr_mel_log_norm_var_f32(const float* power, int64_t ld_power, int64_t stride_power,
+                              const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
+                              float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
+                              int normalize, const int32_t* frames, float* workspace, void* stream);
 /* workspace size of vasr_mel_log_norm_f32 in floats (log-mel rows + per-chunk fp64 partials) */
 int64_t vasr_mel_workspace_floats(int B, int F, int n_mels);
 
@@ -276,6 +287,12 @@ int64_t vasr_mel_workspace_floats(int B, int F, int n_mels);
  * (>= 201), batch stride stride_power (>= F * ldp).  Needs S > 200 (torch's reflect-pad rule). */
 int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
                             float* power, int64_t ldp, int64_t stride_power, void* stream);
+/* samples[b] (device, 200 < samples[b] <= S): utterance b's length inside the zero-padded
+ * (B, S) batch; its reflect padding is taken at its own end, so its first samples[b]/160 + 1
+ * frames equal those of the utterance alone (later frames: ignored by the _var mel pass). */
+int vasr_stft_power_400_var_f32(const float* audio, int64_t ld_audio, int B, int S, const int32_t* samples,
+                                const float* window, float* power, int64_t ldp, int64_t stride_power,
+                                void* stream);
 /* The whole front end for n_fft = 400, hop = 160 with the power spectrum kept on chip: the
  * real FFT above for one 16-frame chunk per workgroup, then in the same workgroup mel + log
  * of the chunk and its per-bin fp64 partials, then the stats / normalisation passes of
@@ -298,6 +315,10 @@ int vasr_pad_frames_f32(const float* x, float* out, int out_frames, int off,
  * x: (B, L, C), out: (B, K, C).
  */
 int vasr_adaptive_pool_f32(const float* x, float* out, int B, int L, int C, int K, void* stream);
+/* Per utterance (device): its first lens[b] rows pooled into ks[b] bins (1 <= ks[b] <= lens[b]
+ * <= L, ks[b] <= K), bins past ks[b] written as 0; x and out keep the strides L and K. */
+int vasr_adaptive_pool_var_f32(const float* x, float* out, int B, int L, int C, int K, const int32_t* lens,
+                               const int32_t* ks, void* stream);
 
 /* Pooled multi-head cross attention core (attention.py:143-160), no mask:
  * out[b,t,h*hd:(h+1)*hd] = softmax(q_bth . k_bh^T / sqrt(hd)) v_bh over the Kp pooled keys.
@@ -306,6 +327,10 @@ int vasr_adaptive_pool_f32(const float* x, float* out, int B, int L, int C, int 
  */
 int vasr_pooled_attention_f32(const float* q, int64_t ld_q, const float* kv, float* out,
                               int B, int L, int Kp, int heads, int head_dim, void* stream);
+/* kps[b] (device, 1 <= kps[b] <= Kp): utterance b attends over its own first kps[b] keys. */
+int vasr_pooled_attention_var_f32(const float* q, int64_t ld_q, const float* kv, float* out,
+                                  int B, int L, int Kp, int heads, int head_dim, const int32_t* kps,
+                                  void* stream);
 
 /* ------------------------------------------------------------------ INT8 fake quantisation (C5)
  * FakeQuantize.forward in eval with calibrated buffers (quantize.py:79-97, :118-133):
@@ -357,6 +382,10 @@ int64_t vasr_ctc_beam_workspace_elems(int L, int W);
 int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse,
                       int32_t* out_tokens, int32_t* out_len, int32_t* out_start,
                       int32_t* out_end, void* stream);
+/* frames[b] (device, 0 <= frames[b] <= L): utterance b collapses its own first frames[b] rows. */
+int vasr_ctc_collapse_var(const int32_t* pred, int B, int L, const int32_t* frames, int blank, int collapse,
+                          int32_t* out_tokens, int32_t* out_len, int32_t* out_start, int32_t* out_end,
+                          void* stream);
 
 #ifdef __cplusplus
 }

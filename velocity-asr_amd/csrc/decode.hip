@@ -45,13 +45,16 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ x
 // prev-token loop, since prev is None after a blank and equals pred[t-1] otherwise.  Kept
 // frames are compacted with a ballot + popcount prefix.  A kept token's end frame is the
 // next run start (the first frame whose value differs), matching decode.py:89-123.
-__global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict__ pred, int L, int blank, int collapse,
+// frames (optional): utterance b collapses its own first frames[b] rows (row stride stays L).
+__global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict__ pred, int ldL, int blank, int collapse,
                                                       int32_t* __restrict__ toks, int32_t* __restrict__ lens,
-                                                      int32_t* __restrict__ st, int32_t* __restrict__ en) {
+                                                      int32_t* __restrict__ st, int32_t* __restrict__ en,
+                                                      const int32_t* __restrict__ frames) {
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
-    const int32_t* p = pred + (int64_t)b * L;
-    int32_t* o = toks + (int64_t)b * L;
+    const int L = frames ? frames[b] : ldL;
+    const int32_t* p = pred + (int64_t)b * ldL;
+    int32_t* o = toks + (int64_t)b * ldL;
     int base = 0;  // tokens kept before this window
     for (int t0 = 0; t0 < L; t0 += 64) {
         const int t = t0 + lane;
@@ -63,19 +66,19 @@ __global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict_
         const int before = __popcll(kmask & ((1ull << lane) - 1ull));
         if (keep) {
             o[base + before] = tok;
-            if (st) st[(int64_t)b * L + base + before] = t;
+            if (st) st[(int64_t)b * ldL + base + before] = t;
         }
         if (st) {
             // a run starting at t closes the previous run; if that run was a kept token, it is
             // the last token kept before t
             const bool run_start = in && t > 0 && prv != tok && prv != blank;
-            if (run_start) en[(int64_t)b * L + base + before - 1] = t;
+            if (run_start) en[(int64_t)b * ldL + base + before - 1] = t;
         }
         base += __popcll(kmask);
     }
     if (lane == 0) {
         lens[b] = base;
-        if (st && L > 0 && p[L - 1] != blank && base > 0) en[(int64_t)b * L + base - 1] = L;
+        if (st && L > 0 && p[L - 1] != blank && base > 0) en[(int64_t)b * ldL + base - 1] = L;
     }
 }
 
@@ -112,17 +115,33 @@ VASR_API int vasr_argmax_f32(const float* logits, int64_t ld, int rows, int V, i
     return launch_status("vasr_argmax_f32");
 }
 
-VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse, int32_t* out_tokens,
-                               int32_t* out_len, int32_t* out_start, int32_t* out_end, void* stream) {
+static int ctc_collapse(const int32_t* pred, int B, int L, const int32_t* frames, int blank, int collapse,
+                        int32_t* out_tokens, int32_t* out_len, int32_t* out_start, int32_t* out_end, void* stream,
+                        const char* who) {
     using namespace vasr;
-    VASR_CHECK_ARG(pred && out_tokens && out_len, "vasr_ctc_collapse: null pointer");
-    VASR_CHECK_ARG((out_start == nullptr) == (out_end == nullptr), "vasr_ctc_collapse: start/end must both be set");
-    VASR_CHECK_ARG(out_start == nullptr || collapse, "vasr_ctc_collapse: timestamps need collapse=1");
-    VASR_CHECK_ARG(B >= 0 && L >= 0, "vasr_ctc_collapse: bad shape");
+    VASR_CHECK_ARG(pred && out_tokens && out_len, "%s: null pointer", who);
+    VASR_CHECK_ARG((out_start == nullptr) == (out_end == nullptr), "%s: start/end must both be set", who);
+    VASR_CHECK_ARG(out_start == nullptr || collapse, "%s: timestamps need collapse=1", who);
+    VASR_CHECK_ARG(B >= 0 && L >= 0, "%s: bad shape", who);
     if (B == 0) return VASR_OK;
     hipLaunchKernelGGL(collapse_kernel, dim3(B), dim3(64), 0, as_stream(stream), pred, L, blank, collapse, out_tokens,
-                       out_len, out_start, out_end);
-    return launch_status("vasr_ctc_collapse");
+                       out_len, out_start, out_end, frames);
+    return launch_status(who);
+}
+
+VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse, int32_t* out_tokens,
+                               int32_t* out_len, int32_t* out_start, int32_t* out_end, void* stream) {
+    return ctc_collapse(pred, B, L, nullptr, blank, collapse, out_tokens, out_len, out_start, out_end, stream,
+                        "vasr_ctc_collapse");
+}
+
+// frames (device): 0 <= frames[b] <= L rows of utterance b (row stride of pred and outputs stays L).
+VASR_API int vasr_ctc_collapse_var(const int32_t* pred, int B, int L, const int32_t* frames, int blank, int collapse,
+                                   int32_t* out_tokens, int32_t* out_len, int32_t* out_start, int32_t* out_end,
+                                   void* stream) {
+    VASR_CHECK_ARG(frames, "vasr_ctc_collapse_var: null frames");
+    return ctc_collapse(pred, B, L, frames, blank, collapse, out_tokens, out_len, out_start, out_end, stream,
+                        "vasr_ctc_collapse_var");
 }
 
 VASR_API int vasr_argmax_keys(const uint64_t* keys, int64_t ld, int slots, int rows, int32_t* out, void* stream) {

@@ -112,7 +112,8 @@ __global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restr
                                                             const int32_t* __restrict__ rowptr,
                                                             const int32_t* __restrict__ col,
                                                             const float* __restrict__ val, float* __restrict__ tmp,
-                                                            double* __restrict__ part, int F, int n_mels) {
+                                                            double* __restrict__ part, int F, int n_mels,
+                                                            const int32_t* __restrict__ frames) {
     __shared__ float rows[kFC * kMaxLdp];
     __shared__ float vals[kFC * kMaxMels];
     __shared__ int rp_s[kMaxMels + 1];
@@ -154,9 +155,11 @@ __global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restr
         tb[i] = v;
     }
     __syncthreads();
+    // frames (optional): only this utterance's own frames enter its statistics
+    const int nfs = frames ? max(min(nf, frames[b] - f0), 0) : nf;
     for (int m = threadIdx.x; m < n_mels; m += blockDim.x) {
         double S = 0.0, Q = 0.0;
-        for (int fl = 0; fl < nf; ++fl) {
+        for (int fl = 0; fl < nfs; ++fl) {
             const double v = (double)vals[fl * n_mels + m];
             S += v;
             Q += v * v;
@@ -175,9 +178,11 @@ __global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restr
 // two memory round trips long instead of six (10.4 -> see DESIGN).
 constexpr int kStatPh = 12;
 __global__ __launch_bounds__(1024) void mel_chunk_stats_kernel(const double* __restrict__ part, float* __restrict__ stats,
-                                                               int nch, int F, int n_mels, int normalize) {
+                                                               int nch, int F, int n_mels, int normalize,
+                                                               const int32_t* __restrict__ frames) {
     __shared__ double red[2][kStatPh][kMaxMels];
     const int b = blockIdx.x;
+    if (frames) F = frames[b];  // chunks past the utterance's end hold zero partials
     const int m = threadIdx.x % n_mels, ph = threadIdx.x / n_mels;  // phases of n_mels threads (n_mels <= 85)
     const int nph = min(kStatPh, (int)blockDim.x / n_mels);
     if (ph < nph) {
@@ -220,11 +225,12 @@ __global__ __launch_bounds__(1024) void mel_chunk_stats_kernel(const double* __r
 __global__ __launch_bounds__(256) void mel_chunk_norm_kernel(const float* __restrict__ tmp,
                                                              const float* __restrict__ stats, float* __restrict__ out,
                                                              int64_t out_stride, int frame_off, int F, int n_mels,
-                                                             int normalize) {
+                                                             int normalize, const int32_t* __restrict__ frames) {
     __shared__ float st_s[2 * kMaxMels];
     const int b = blockIdx.y, c = blockIdx.x;
     const int f0 = c * kFC;
     const int nf = min(kFC, F - f0);
+    const int nv = frames ? max(min(nf, frames[b] - f0), 0) : nf;  // frames past the utterance's end -> 0
     for (int i = threadIdx.x; i < 2 * n_mels; i += blockDim.x) st_s[i] = stats[(int64_t)b * n_mels * 2 + i];
     __syncthreads();
     const float* tb = tmp + ((int64_t)b * F + f0) * n_mels;
@@ -232,7 +238,7 @@ __global__ __launch_bounds__(256) void mel_chunk_norm_kernel(const float* __rest
     for (int i = threadIdx.x; i < nf * n_mels; i += blockDim.x) {
         const int m = i % n_mels;
         const float x = tb[i];
-        dst[i] = normalize ? (x - st_s[2 * m]) / st_s[2 * m + 1] : x;
+        dst[i] = i >= nv * n_mels ? 0.0f : normalize ? (x - st_s[2 * m]) / st_s[2 * m + 1] : x;
     }
 }
 
@@ -252,15 +258,16 @@ __global__ void pad_frames_kernel(const float* __restrict__ x, float* __restrict
 // Stats + normalisation passes of the chunked front end over the workspace written by a
 // chunk-log pass (mel_chunk_log_kernel, or the fused STFT + log-mel of stft.hip).
 int mel_chunk_finish(float* workspace, float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
-                     int normalize, hipStream_t s) {
+                     int normalize, hipStream_t s, const int32_t* frames) {
     const int nch = (F + kFC - 1) / kFC;
     double* part = reinterpret_cast<double*>(workspace + (((int64_t)B * F * n_mels + 1) & ~(int64_t)1));
     float* stats = reinterpret_cast<float*>(part + (int64_t)B * nch * n_mels * 2);
-    hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(1024), 0, s, part, stats, nch, F, n_mels, normalize);
+    hipLaunchKernelGGL(mel_chunk_stats_kernel, dim3(B), dim3(1024), 0, s, part, stats, nch, F, n_mels, normalize,
+                       frames);
     int rc = launch_status("mel stats");
     if (rc) return rc;
     hipLaunchKernelGGL(mel_chunk_norm_kernel, dim3(nch, B), dim3(256), 0, s, workspace, stats, out, out_stride,
-                       frame_off, F, n_mels, normalize);
+                       frame_off, F, n_mels, normalize, frames);
     return launch_status("mel norm");
 }
 
@@ -280,14 +287,14 @@ VASR_API int vasr_reflect_pad_f32(const float* audio, int64_t ld_audio, float* x
     return launch_status("vasr_reflect_pad_f32");
 }
 
-VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t stride_power,
-                                   const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val, float* out,
-                                   int64_t out_stride, int frame_off, int B, int F, int n_mels, int normalize,
-                                   float* workspace, void* stream) {
+static int mel_log_norm(const float* power, int64_t ld_power, int64_t stride_power, const int32_t* fb_rowptr,
+                        const int32_t* fb_col, const float* fb_val, float* out, int64_t out_stride, int frame_off,
+                        int B, int F, int n_mels, int normalize, float* workspace, const int32_t* frames,
+                        void* stream, const char* who) {
     using namespace vasr;
-    VASR_CHECK_ARG(power && fb_rowptr && fb_col && fb_val && out && workspace, "vasr_mel_log_norm_f32: null pointer");
-    VASR_CHECK_ARG(B >= 0 && F >= 1 && n_mels >= 1 && frame_off >= 0, "vasr_mel_log_norm_f32: bad shape");
-    VASR_CHECK_ARG(out_stride >= (int64_t)(F + frame_off) * n_mels, "vasr_mel_log_norm_f32: out_stride too small");
+    VASR_CHECK_ARG(power && fb_rowptr && fb_col && fb_val && out && workspace, "%s: null pointer", who);
+    VASR_CHECK_ARG(B >= 0 && F >= 1 && n_mels >= 1 && frame_off >= 0, "%s: bad shape", who);
+    VASR_CHECK_ARG(out_stride >= (int64_t)(F + frame_off) * n_mels, "%s: out_stride too small", who);
     if (B == 0) return VASR_OK;
     hipStream_t s = as_stream(stream);
     if (ld_power <= kMaxLdp && n_mels <= kMaxMels) {
@@ -296,19 +303,41 @@ VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t
         const int nch = (F + kFC - 1) / kFC;
         double* part = reinterpret_cast<double*>(workspace + (((int64_t)B * F * n_mels + 1) & ~(int64_t)1));
         hipLaunchKernelGGL(mel_chunk_log_kernel, dim3(nch, B), dim3(256), 0, s, power, ld_power, stride_power,
-                           fb_rowptr, fb_col, fb_val, workspace, part, F, n_mels);
-        int rc = launch_status("vasr_mel_log_norm_f32/log");
+                           fb_rowptr, fb_col, fb_val, workspace, part, F, n_mels, frames);
+        int rc = launch_status(who);
         if (rc) return rc;
-        return mel_chunk_finish(workspace, out, out_stride, frame_off, B, F, n_mels, normalize, s);
+        return mel_chunk_finish(workspace, out, out_stride, frame_off, B, F, n_mels, normalize, s, frames);
     }
+    VASR_CHECK_ARG(!frames, "%s: per-utterance frame counts need ld_power <= %d and n_mels <= %d", who, kMaxLdp,
+                   kMaxMels);
     const int64_t total = (int64_t)B * F * n_mels;
     hipLaunchKernelGGL(mel_log_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, power, ld_power,
                        stride_power, fb_rowptr, fb_col, fb_val, workspace, B, F, n_mels);
-    int rc = launch_status("vasr_mel_log_norm_f32/log");
+    int rc = launch_status(who);
     if (rc) return rc;
     hipLaunchKernelGGL(mel_norm_kernel, dim3((n_mels + 15) / 16, B), dim3(256), 0, s, workspace, out, out_stride,
                        frame_off, F, n_mels, normalize);
-    return launch_status("vasr_mel_log_norm_f32/norm");
+    return launch_status(who);
+}
+
+VASR_API int vasr_mel_log_norm_f32(const float* power, int64_t ld_power, int64_t stride_power,
+                                   const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val, float* out,
+                                   int64_t out_stride, int frame_off, int B, int F, int n_mels, int normalize,
+                                   float* workspace, void* stream) {
+    return mel_log_norm(power, ld_power, stride_power, fb_rowptr, fb_col, fb_val, out, out_stride, frame_off, B, F,
+                        n_mels, normalize, workspace, nullptr, stream, "vasr_mel_log_norm_f32");
+}
+
+// frames[b] <= F (device): utterance b's own frame count.  Its statistics cover those frames
+// only (the same sums, in the same order, as the utterance alone) and its frames past them are
+// written as 0 (the zero padding the stride-2 temporal conv then sees).
+VASR_API int vasr_mel_log_norm_var_f32(const float* power, int64_t ld_power, int64_t stride_power,
+                                       const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
+                                       float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
+                                       int normalize, const int32_t* frames, float* workspace, void* stream) {
+    VASR_CHECK_ARG(frames, "vasr_mel_log_norm_var_f32: null frames");
+    return mel_log_norm(power, ld_power, stride_power, fb_rowptr, fb_col, fb_val, out, out_stride, frame_off, B, F,
+                        n_mels, normalize, workspace, frames, stream, "vasr_mel_log_norm_var_f32");
 }
 
 VASR_API int64_t vasr_mel_workspace_floats(int B, int F, int n_mels) {

@@ -118,7 +118,8 @@ constexpr int kMelMaxNnz = 1024, kMelMaxBins = 85;
 
 template <int FPB, bool MEL>
 __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __restrict__ audio, int64_t ld_audio,
-                                                             int S, int F, const float* __restrict__ window,
+                                                             int S, const int32_t* __restrict__ samples, int F,
+                                                             const float* __restrict__ window,
                                                              float* __restrict__ power, int64_t ldp,
                                                              int64_t stridep, MelArgs ma) {
     __shared__ cf tw[kHalf + kBins];  // W200^j, then W400^k
@@ -141,10 +142,13 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     cf twv[kTwIt];
 #pragma unroll
     for (int it = 0; it < kTwIt; ++it) twv[it] = twg[min(tid + it * 256, kHalf + kBins - 1)];
-    auto reflect = [S](int j) {
+    // samples (optional): this utterance's own length; its reflect padding is taken at its own
+    // end (frames past its last one read clamped data and are ignored downstream)
+    const int Sb = samples ? samples[b] : S;
+    auto reflect = [Sb](int j) {
         j = j < 0 ? -j : j;
-        j = j >= S ? 2 * (S - 1) - j : j;
-        return min(max(j, 0), S - 1);  // frames past F read clamped data, never stored
+        j = j >= Sb ? 2 * (Sb - 1) - j : j;
+        return min(max(j, 0), Sb - 1);  // frames past F read clamped data, never stored
     };
     float x0[kPackIt], x1[kPackIt];
     float2 w[kPackIt];
@@ -266,18 +270,36 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
 }  // namespace
 }  // namespace vasr
 
-VASR_API int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
-                                     float* power, int64_t ldp, int64_t stride_power, void* stream) {
+static int stft_power_400(const float* audio, int64_t ld_audio, int B, int S, const int32_t* samples,
+                          const float* window, float* power, int64_t ldp, int64_t stride_power, void* stream,
+                          const char* who) {
     using namespace vasr;
-    VASR_CHECK_ARG(audio && window && power, "vasr_stft_power_400_f32: null pointer");
-    VASR_CHECK_ARG(((uintptr_t)window & 7) == 0, "vasr_stft_power_400_f32: window must be 8-byte aligned");
-    VASR_CHECK_ARG(B >= 0 && S > kNfft / 2 && ld_audio >= S && ldp >= kBins, "vasr_stft_power_400_f32: bad shape");
+    VASR_CHECK_ARG(audio && window && power, "%s: null pointer", who);
+    VASR_CHECK_ARG(((uintptr_t)window & 7) == 0, "%s: window must be 8-byte aligned", who);
+    VASR_CHECK_ARG(B >= 0 && S > kNfft / 2 && ld_audio >= S && ldp >= kBins, "%s: bad shape", who);
     const int F = (S + 2 * (kNfft / 2) - kNfft) / kHop + 1;
-    VASR_CHECK_ARG(stride_power >= (int64_t)F * ldp, "vasr_stft_power_400_f32: stride_power too small");
+    VASR_CHECK_ARG(stride_power >= (int64_t)F * ldp, "%s: stride_power too small", who);
     if (B == 0) return VASR_OK;
     hipLaunchKernelGGL((stft_power_400_kernel<kFPB, false>), dim3((F + kFPB - 1) / kFPB, B), dim3(256), 0,
-                       as_stream(stream), audio, ld_audio, S, F, window, power, ldp, stride_power, MelArgs{});
-    return launch_status("vasr_stft_power_400_f32");
+                       as_stream(stream), audio, ld_audio, S, samples, F, window, power, ldp, stride_power, MelArgs{});
+    return launch_status(who);
+}
+
+VASR_API int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
+                                     float* power, int64_t ldp, int64_t stride_power, void* stream) {
+    return stft_power_400(audio, ld_audio, B, S, nullptr, window, power, ldp, stride_power, stream,
+                          "vasr_stft_power_400_f32");
+}
+
+// Utterances of different lengths in one zero-padded (B, S) batch: samples[b] <= S is
+// utterance b's own length (> 200), on the device.  Frames f < samples[b] / 160 + 1 are those
+// of the utterance alone; later frames are ignored by the _var mel pass.
+VASR_API int vasr_stft_power_400_var_f32(const float* audio, int64_t ld_audio, int B, int S, const int32_t* samples,
+                                         const float* window, float* power, int64_t ldp, int64_t stride_power,
+                                         void* stream) {
+    VASR_CHECK_ARG(samples, "vasr_stft_power_400_var_f32: null samples");
+    return stft_power_400(audio, ld_audio, B, S, samples, window, power, ldp, stride_power, stream,
+                          "vasr_stft_power_400_var_f32");
 }
 
 VASR_API int vasr_stft_logmel_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
@@ -298,8 +320,8 @@ VASR_API int vasr_stft_logmel_400_f32(const float* audio, int64_t ld_audio, int 
     const int nch = (F + kMelChunk - 1) / kMelChunk;
     MelArgs ma{fb_rowptr, fb_col, fb_val, workspace,
                reinterpret_cast<double*>(workspace + (((int64_t)B * F * n_mels + 1) & ~(int64_t)1)), n_mels};
-    hipLaunchKernelGGL((stft_power_400_kernel<kMelChunk, true>), dim3(nch, B), dim3(256), 0, s, audio, ld_audio, S, F,
-                       window, nullptr, 0, 0, ma);
+    hipLaunchKernelGGL((stft_power_400_kernel<kMelChunk, true>), dim3(nch, B), dim3(256), 0, s, audio, ld_audio, S,
+                       nullptr, F, window, nullptr, 0, 0, ma);
     const int rc = launch_status("vasr_stft_logmel_400_f32");
     if (rc) return rc;
     return mel_chunk_finish(workspace, out, out_stride, frame_off, B, F, n_mels, normalize, s);

@@ -31,8 +31,9 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // mel.hip: the stats + normalisation passes of the chunked log-mel front end (kFC = 16 frames
 // per chunk) over a workspace laid out as vasr_mel_workspace_floats describes.
 constexpr int kMelChunk = 16;
+// frames (optional, device): per-utterance frame counts <= F (vasr_mel_log_norm_var_f32)
 int mel_chunk_finish(float* workspace, float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
-                     int normalize, hipStream_t s);
+                     int normalize, hipStream_t s, const int32_t* frames = nullptr);
 
 constexpr int kWave = 64;
 

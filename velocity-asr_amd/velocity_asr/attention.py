@@ -9,7 +9,7 @@ gate, local and global branches in registers (no (B, L, 2D) concat, no gate tens
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
@@ -18,6 +18,11 @@ from . import _lib, ops
 from . import quantize as Q
 from ._prep import cached
 from .ssm import GlobalSSM
+
+
+def _device_ints(values: Sequence[int], device) -> torch.Tensor:
+    """Host sizes -> the int32 (B,) device array the _var kernels read."""
+    return torch.tensor([int(v) for v in values], dtype=torch.int32).to(device)
 
 
 class AdaptivePool(nn.Module):
@@ -35,14 +40,24 @@ class AdaptivePool(nn.Module):
         k1 = prev_pool_size if prev_pool_size else max(64, seq_len // 8)
         return min(64, max(16, k1 // 4))
 
-    def forward(self, x: torch.Tensor, prev_pool_size: Optional[int] = None) -> Tuple[torch.Tensor, int]:
+    def forward(self, x: torch.Tensor, prev_pool_size=None, lengths: Optional[Sequence[int]] = None):
+        """(B, L, D) -> ((B, K, D), K).  lengths: per-utterance valid rows of a zero-padded batch
+        (prev_pool_size then per utterance too): each utterance is pooled to the size it gets
+        alone, rows past it are junk nobody reads, and the sizes are returned as a list."""
         B, L, D = x.shape
-        pool_size = min(self._compute_pool_size(L, prev_pool_size), L)
-        pooled = ops.adaptive_pool(x, pool_size)
+        if lengths is None:
+            pool_size = min(self._compute_pool_size(L, prev_pool_size), L)
+            pooled = ops.adaptive_pool(x, pool_size)
+        else:
+            prev = prev_pool_size if prev_pool_size is not None else [None] * B
+            sizes = [min(self._compute_pool_size(n, p), n) for n, p in zip(lengths, prev)]
+            pool_size = max(sizes)
+            pooled = ops.adaptive_pool(x, pool_size, lens=_device_ints(lengths, x.device),
+                                       ks=_device_ints(sizes, x.device))
         w, b, qp = Q.linear_parts(self.pool_proj)
         out = ops.gemm(pooled.view(B * pool_size, D), w, b, qparams=qp)
         Q.record(self.pool_proj, out)
-        return out.view(B, pool_size, D), pool_size
+        return out.view(B, pool_size, D), (pool_size if lengths is None else sizes)
 
 
 class MultiHeadAttention(nn.Module):
@@ -81,7 +96,8 @@ class MultiHeadAttention(nn.Module):
         return cached(self, "kv", Q.deps(self.k_proj) + Q.deps(self.v_proj), build)
 
     def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
-                mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+                mask: Optional[torch.Tensor] = None, key_lengths: Optional[Sequence[int]] = None) -> torch.Tensor:
+        """key_lengths: per-utterance valid keys of a padded (B, Kp, D) key set."""
         if mask is not None:
             raise NotImplementedError("velocity_asr (MI355X build): attention masks are not supported "
                                       "(the reference path never passes one)")
@@ -101,7 +117,8 @@ class MultiHeadAttention(nn.Module):
                 ops.gemm(src.reshape(B * Kp, D), w, b, out=kv[:, sl], qparams=qp)
         Q.record(self.k_proj, kv[:, :A])
         Q.record(self.v_proj, kv[:, A:])
-        o = ops.pooled_attention(q, kv, B, Lq, Kp, self.num_heads)
+        o = ops.pooled_attention(q, kv, B, Lq, Kp, self.num_heads,
+                                 kps=None if key_lengths is None else _device_ints(key_lengths, q.device))
         wo, bo, qpo = Q.linear_parts(self.out_proj)
         out = ops.gemm(o, wo, bo, qparams=qpo)
         Q.record(self.out_proj, out)
@@ -188,11 +205,16 @@ class HierarchicalGlobalContext(nn.Module):
         self.norm2 = nn.LayerNorm(d_model)
         self.fusion = GatedFusion(d_model=d_model)
 
-    def forward(self, local_features: torch.Tensor) -> torch.Tensor:
-        x_pool1, pool_size1 = self.pool1(local_features)
+    def forward(self, local_features: torch.Tensor, lengths: Optional[Sequence[int]] = None) -> torch.Tensor:
+        """lengths: per-utterance token counts of a zero-padded batch (None: all L).  Pooling
+        sizes and attention keys then follow each utterance's own length; the global SSM is
+        causal, so the junk rows past an utterance's pooled tokens never reach them."""
+        x_pool1, pool_size1 = self.pool1(local_features, lengths=lengths)
         x_ssm = self.global_ssm(x_pool1)
-        x_pool2, _ = self.pool2(x_ssm, prev_pool_size=pool_size1)
+        x_pool2, pool_size2 = self.pool2(x_ssm, prev_pool_size=pool_size1,
+                                         lengths=None if lengths is None else pool_size1)
         x_pool2 = ops.layer_norm(x_pool2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         query = ops.layer_norm(local_features, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-        global_context = self.cross_attention(query=query, key=x_pool2, value=x_pool2)
+        global_context = self.cross_attention(query=query, key=x_pool2, value=x_pool2,
+                                              key_lengths=None if lengths is None else pool_size2)
         return self.fusion(local_features, global_context)

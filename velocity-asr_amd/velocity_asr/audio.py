@@ -240,11 +240,13 @@ def _target_device(t: torch.Tensor) -> torch.device:
 
 def compute_mel_spectrogram(audio: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
                             hop_length: int = HOP_LENGTH, n_mels: int = N_MELS,
-                            normalize: bool = True) -> torch.Tensor:
+                            normalize: bool = True, lengths=None) -> torch.Tensor:
     """Log-mel spectrogram (reference audio.py:65-143) on the MI355X.
 
     audio (samples,) or (batch, samples) -> (frames, n_mels) or (batch, frames, n_mels),
-    frames = samples // hop_length + 1, on the input's device.
+    frames = samples // hop_length + 1, on the input's device.  lengths (extension): the
+    per-clip sample counts of a batch of clips of different lengths zero-padded to a common
+    length (see mel_on_device).
     """
     squeeze = audio.dim() == 1
     if squeeze:
@@ -253,7 +255,7 @@ def compute_mel_spectrogram(audio: torch.Tensor, sample_rate: int = SAMPLE_RATE,
         raise ValueError(f"compute_mel_spectrogram: expected (samples,) or (batch, samples), got {tuple(audio.shape)}")
     dev = _target_device(audio)
     x = audio.to(device=dev, dtype=torch.float32).contiguous()
-    mel = mel_on_device(x, sample_rate, n_fft, hop_length, n_mels, normalize)
+    mel = mel_on_device(x, sample_rate, n_fft, hop_length, n_mels, normalize, lengths=lengths)
     if audio.device.type != "cuda":
         mel = mel.to(audio.device)
     return mel.squeeze(0) if squeeze else mel
@@ -270,8 +272,14 @@ _STFT_FFT = _STFT_MODE != "gemm"
 
 
 def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
-                  hop_length: int = HOP_LENGTH, n_mels: int = N_MELS, normalize: bool = True) -> torch.Tensor:
-    """(B, S) float32 HIP tensor -> (B, F, n_mels) on the same device."""
+                  hop_length: int = HOP_LENGTH, n_mels: int = N_MELS, normalize: bool = True,
+                  lengths=None) -> torch.Tensor:
+    """(B, S) float32 HIP tensor -> (B, F, n_mels) on the same device.
+
+    lengths (extension): per-utterance sample counts of a batch of clips of different lengths,
+    zero-padded to S.  Utterance b's first audio_to_frames(lengths[b]) frames are then those of
+    the clip alone (its reflect padding and its normalisation statistics are its own) and its
+    later frames are 0; pass the frame counts on as VELOCITYASR(..., frames=)."""
     B, S = x.shape
     pad = n_fft // 2
     if S <= pad:
@@ -280,6 +288,18 @@ def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = 
         raise NotImplementedError("HIP front end needs n_fft and hop_length to be multiples of 4")
     n_frames = (S + 2 * pad - n_fft) // hop_length + 1
     tb = _tables(x.device, n_fft, n_mels, sample_rate)
+    if lengths is not None:
+        lengths = [int(v) for v in lengths]
+        if len(lengths) != B or not all(pad < v <= S for v in lengths):
+            raise RuntimeError(f"compute_mel_spectrogram: lengths must be {B} sample counts in ({pad}, {S}], "
+                               f"got {lengths}")
+        if not (n_fft == 400 and hop_length == 160 and _STFT_FFT and n_mels <= 85):
+            raise NotImplementedError("per-utterance lengths need the FFT front end (n_fft 400, hop 160, n_mels <= 85)")
+        samples = torch.tensor(lengths, dtype=torch.int32).to(x.device)
+        frames = torch.tensor([(v + 2 * pad - n_fft) // hop_length + 1 for v in lengths], dtype=torch.int32).to(x.device)
+        power = ops.stft_power_400(x, tb.window, samples=samples)
+        return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize,
+                                frames=frames)
     if n_fft == 400 and hop_length == 160 and _STFT_FFT:
         if _STFT_MODE == "fused" and n_mels <= 85:  # FFT + log-mel in one launch (power stays in LDS)
             return ops.stft_logmel_400(x, tb.window, tb.fb_csr, n_mels, normalize)

@@ -175,34 +175,51 @@ class VELOCITYASR(nn.Module):
                 nn.init.ones_(module.weight)
                 nn.init.zeros_(module.bias)
 
-    def forward(self, mel_spectrogram: torch.Tensor, return_features: bool = False):
-        """(B, frames, mel_bins) -> CTC logits (B, (frames + 1) // 2, vocab_size)."""
+    def _token_lengths(self, frames, n_frames: int):
+        """Per-utterance token counts of a zero-padded batch (frames: its per-utterance mel frame
+        counts, each <= n_frames, frames past them zero), or None for a uniform batch."""
+        if frames is None:
+            return None
+        frames = [int(f) for f in frames]
+        if not all(1 <= f <= n_frames for f in frames):
+            raise ValueError(f"frames: each utterance needs 1..{n_frames} frames, got {frames}")
+        return [self.temporal_binding.output_length(f) for f in frames]
+
+    def forward(self, mel_spectrogram: torch.Tensor, return_features: bool = False, frames=None):
+        """(B, frames, mel_bins) -> CTC logits (B, (frames + 1) // 2, vocab_size).
+
+        frames (extension): per-utterance frame counts of a batch of utterances of different
+        lengths, zero-padded to a common length (velocity_asr.audio.mel_on_device(...,
+        lengths=) writes such a batch).  Every utterance's logits over its own
+        get_output_length(frames[b]) rows are then those it gets alone; later rows are junk."""
         if mel_spectrogram.device.type != "cuda":
             _lib.require_device()
             raise RuntimeError("velocity_asr (MI355X build): move the model and input to the HIP device "
                                "(model.to('cuda'), mel.to('cuda')); there is no CPU execution path")
         mel = mel_spectrogram.to(torch.float32)
+        lengths = self._token_lengths(frames, mel.shape[1])
         with torch.no_grad():
             x = self.temporal_binding(mel)
             local_features = self.local_ssm(x)
-            fused_features = self.global_context(local_features)
+            fused_features = self.global_context(local_features, lengths=lengths)
             logits = self.ctc_head(fused_features)
         if return_features:
             return logits, {"temporal_binding": x, "local_features": local_features,
                             "fused_features": fused_features}
         return logits
 
-    def token_ids(self, mel_spectrogram: torch.Tensor) -> torch.Tensor:
+    def token_ids(self, mel_spectrogram: torch.Tensor, frames=None) -> torch.Tensor:
         """argmax(forward(mel), -1) as (B, L) int32 on the device, without materialising logits
         (the CTC head's GEMM reduces each row in its epilogue).  Identical to the argmax of
         forward()'s logits: same GEMM, same accumulation order."""
         if mel_spectrogram.device.type != "cuda":
             _lib.require_device()
             raise RuntimeError("velocity_asr (MI355X build): token_ids needs HIP tensors")
+        lengths = self._token_lengths(frames, mel_spectrogram.shape[1])
         with torch.no_grad():
             x = self.temporal_binding(mel_spectrogram.to(torch.float32))
             x = self.local_ssm(x)
-            x = self.global_context(x)
+            x = self.global_context(x, lengths=lengths)
             return self.ctc_head.argmax(x)
 
     def get_output_length(self, input_length: int) -> int:

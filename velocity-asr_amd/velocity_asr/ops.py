@@ -516,8 +516,18 @@ def reflect_pad(audio: torch.Tensor, pad: int, ld_out: int) -> torch.Tensor:
     return xp
 
 
-def stft_power_400(audio: torch.Tensor, window: torch.Tensor) -> torch.Tensor:
-    """(B, S) audio -> (B, S // 160 + 1, 201) |STFT|^2 (n_fft 400, hop 160, reflect pad, Hann)."""
+def _lens(name: str, t: Optional[torch.Tensor], B: int, device) -> Optional[torch.Tensor]:
+    """Per-utterance size array of a zero-padded batch: a contiguous int32 (B,) tensor on the device."""
+    if t is None:
+        return None
+    if t.device != device or t.dtype != torch.int32 or tuple(t.shape) != (B,) or not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous int32 ({B},) tensor on {device}")
+    return t
+
+
+def stft_power_400(audio: torch.Tensor, window: torch.Tensor, samples: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B, S) audio -> (B, S // 160 + 1, 201) |STFT|^2 (n_fft 400, hop 160, reflect pad, Hann).
+    samples: per-utterance lengths (int32 (B,), each in (200, S]) of a zero-padded batch."""
     _cuda_f32("stft_power_400.audio", audio)
     _cuda_f32("stft_power_400.window", window)
     audio = audio.contiguous()
@@ -526,8 +536,15 @@ def stft_power_400(audio: torch.Tensor, window: torch.Tensor) -> torch.Tensor:
         raise ValueError(f"stft_power_400: window must have 400 entries, got {window.numel()}")
     F = S // 160 + 1
     power = torch.empty((B, F, 201), device=audio.device, dtype=torch.float32)
-    check(L.lib().vasr_stft_power_400_f32(audio.data_ptr(), S, B, S, window.contiguous().data_ptr(), power.data_ptr(),
-                                          201, F * 201, stream_of(audio)), "vasr_stft_power_400_f32")
+    samples = _lens("stft_power_400.samples", samples, B, audio.device)
+    if samples is None:
+        check(L.lib().vasr_stft_power_400_f32(audio.data_ptr(), S, B, S, window.contiguous().data_ptr(),
+                                              power.data_ptr(), 201, F * 201, stream_of(audio)),
+              "vasr_stft_power_400_f32")
+    else:
+        check(L.lib().vasr_stft_power_400_var_f32(audio.data_ptr(), S, B, S, samples.data_ptr(),
+                                                  window.contiguous().data_ptr(), power.data_ptr(), 201, F * 201,
+                                                  stream_of(audio)), "vasr_stft_power_400_var_f32")
     return power
 
 
@@ -549,13 +566,22 @@ def stft_logmel_400(audio: torch.Tensor, window: torch.Tensor, fb_csr, n_mels: i
 
 
 def mel_log_norm(power: torch.Tensor, ld_power: int, stride_power: int, fb_csr, B: int, F: int, n_mels: int,
-                 normalize: bool) -> torch.Tensor:
+                 normalize: bool, frames: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """frames: per-utterance frame counts (int32 (B,), each <= F); frames past them are 0."""
     rowptr, col, val = fb_csr
     out = torch.empty((B, F, n_mels), device=power.device, dtype=torch.float32)
     ws = torch.empty(int(L.lib().vasr_mel_workspace_floats(B, F, n_mels)), device=power.device, dtype=torch.float32)
-    check(L.lib().vasr_mel_log_norm_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(), col.data_ptr(),
-                                        val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F, n_mels, int(normalize),
-                                        ws.data_ptr(), stream_of(power)), "vasr_mel_log_norm_f32")
+    frames = _lens("mel_log_norm.frames", frames, B, power.device)
+    if frames is None:
+        check(L.lib().vasr_mel_log_norm_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(),
+                                            col.data_ptr(), val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F,
+                                            n_mels, int(normalize), ws.data_ptr(), stream_of(power)),
+              "vasr_mel_log_norm_f32")
+    else:
+        check(L.lib().vasr_mel_log_norm_var_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(),
+                                                col.data_ptr(), val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F,
+                                                n_mels, int(normalize), frames.data_ptr(), ws.data_ptr(),
+                                                stream_of(power)), "vasr_mel_log_norm_var_f32")
     return out
 
 
@@ -569,17 +595,30 @@ def pad_frames(x: torch.Tensor, out_frames: int, off: int) -> torch.Tensor:
     return out
 
 
-def adaptive_pool(x: torch.Tensor, K: int) -> torch.Tensor:
+def adaptive_pool(x: torch.Tensor, K: int, lens: Optional[torch.Tensor] = None,
+                  ks: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B, L, C) -> (B, K, C) adaptive average pooling over time; with lens / ks (int32 (B,))
+    utterance b pools its first lens[b] rows into ks[b] bins, later bins 0."""
     _cuda_f32("adaptive_pool.x", x)
     x = x.contiguous()
     B, Lq, C = x.shape
     out = torch.empty((B, K, C), device=x.device, dtype=torch.float32)
-    check(L.lib().vasr_adaptive_pool_f32(x.data_ptr(), out.data_ptr(), B, Lq, C, K, stream_of(x)),
-          "vasr_adaptive_pool_f32")
+    if (lens is None) != (ks is None):
+        raise ValueError("adaptive_pool: lens and ks go together")
+    if lens is None:
+        check(L.lib().vasr_adaptive_pool_f32(x.data_ptr(), out.data_ptr(), B, Lq, C, K, stream_of(x)),
+              "vasr_adaptive_pool_f32")
+    else:
+        lens = _lens("adaptive_pool.lens", lens, B, x.device)
+        ks = _lens("adaptive_pool.ks", ks, B, x.device)
+        check(L.lib().vasr_adaptive_pool_var_f32(x.data_ptr(), out.data_ptr(), B, Lq, C, K, lens.data_ptr(),
+                                                 ks.data_ptr(), stream_of(x)), "vasr_adaptive_pool_var_f32")
     return out
 
 
-def pooled_attention(q: torch.Tensor, kv: torch.Tensor, B: int, Lq: int, Kp: int, heads: int) -> torch.Tensor:
+def pooled_attention(q: torch.Tensor, kv: torch.Tensor, B: int, Lq: int, Kp: int, heads: int,
+                     kps: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """kps: per-utterance key counts (int32 (B,), each in [1, Kp])."""
     _cuda_f32("pooled_attention.q", q)
     _cuda_f32("pooled_attention.kv", kv)
     M, A, ld_q = _rows("pooled_attention.q", q)
@@ -587,8 +626,14 @@ def pooled_attention(q: torch.Tensor, kv: torch.Tensor, B: int, Lq: int, Kp: int
     if kv.shape != (B * Kp, 2 * A) or M != B * Lq or A % heads:
         raise ValueError("pooled_attention: inconsistent shapes")
     out = torch.empty((M, A), device=q.device, dtype=torch.float32)
-    check(L.lib().vasr_pooled_attention_f32(q.data_ptr(), ld_q, kv.data_ptr(), out.data_ptr(), B, Lq, Kp, heads,
-                                            A // heads, stream_of(q)), "vasr_pooled_attention_f32")
+    kps = _lens("pooled_attention.kps", kps, B, q.device)
+    if kps is None:
+        check(L.lib().vasr_pooled_attention_f32(q.data_ptr(), ld_q, kv.data_ptr(), out.data_ptr(), B, Lq, Kp, heads,
+                                                A // heads, stream_of(q)), "vasr_pooled_attention_f32")
+    else:
+        check(L.lib().vasr_pooled_attention_var_f32(q.data_ptr(), ld_q, kv.data_ptr(), out.data_ptr(), B, Lq, Kp,
+                                                    heads, A // heads, kps.data_ptr(), stream_of(q)),
+              "vasr_pooled_attention_var_f32")
     return out
 
 
@@ -607,10 +652,10 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
 
 
 def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, timestamps: bool = False,
-                 out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+                 out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, frames: Optional[torch.Tensor] = None):
     """Device-side greedy CTC collapse of (B, L) int32 predictions.  out = (tokens (B, L),
     lengths (B,)): contiguous int32 buffers to write into (e.g. row slices of a graph's
-    static output)."""
+    static output).  frames: per-utterance row counts (int32 (B,)) of a padded batch."""
     if pred.device.type != "cuda" or pred.dtype != torch.int32:
         raise TypeError("ctc_collapse: expected a cuda int32 tensor")
     pred = pred.contiguous()
@@ -628,8 +673,14 @@ def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, time
     if timestamps:
         st = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
         en = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
-    check(L.lib().vasr_ctc_collapse(pred.data_ptr(), B, Lq, int(blank), int(collapse), toks.data_ptr(),
-                                    lens.data_ptr(), ptr(st), ptr(en), stream_of(pred)), "vasr_ctc_collapse")
+    frames = _lens("ctc_collapse.frames", frames, B, pred.device)
+    if frames is None:
+        check(L.lib().vasr_ctc_collapse(pred.data_ptr(), B, Lq, int(blank), int(collapse), toks.data_ptr(),
+                                        lens.data_ptr(), ptr(st), ptr(en), stream_of(pred)), "vasr_ctc_collapse")
+    else:
+        check(L.lib().vasr_ctc_collapse_var(pred.data_ptr(), B, Lq, frames.data_ptr(), int(blank), int(collapse),
+                                            toks.data_ptr(), lens.data_ptr(), ptr(st), ptr(en), stream_of(pred)),
+              "vasr_ctc_collapse_var")
     return toks, lens, st, en
 
 

@@ -26,15 +26,23 @@ FUSED_ARGMAX = os.environ.get("VASR_FUSED_ARGMAX", "1") != "0"
 
 
 def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0,
-                       out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                       out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                       lengths: Optional[List[int]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """(B, S) float32 HIP audio -> (tokens (B, L) int32, lengths (B,) int32), all on the device.
-    out = (tokens, lengths) buffers to write the collapsed result into."""
-    mel = mel_on_device(audio, SAMPLE_RATE, N_FFT, HOP_LENGTH, model.config.mel_bins)
+    out = (tokens, lengths) buffers to write the collapsed result into.  lengths: per-clip
+    sample counts of clips of different lengths zero-padded to S (each clip's tokens are then
+    those it gets alone: mel statistics, pooling sizes, attention keys and the collapse follow
+    its own length, and the SSM stacks are causal)."""
+    mel = mel_on_device(audio, SAMPLE_RATE, N_FFT, HOP_LENGTH, model.config.mel_bins, lengths=lengths)
+    frames = None if lengths is None else [int(v) // HOP_LENGTH + 1 for v in lengths]
     if FUSED_ARGMAX:
-        pred = model.token_ids(mel)  # CTC head GEMM with the row argmax fused: no logits in HBM
+        pred = model.token_ids(mel, frames=frames)  # CTC head GEMM with the row argmax fused: no logits in HBM
     else:
-        pred = ops.argmax(model(mel))
-    toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False, out=out)
+        pred = ops.argmax(model(mel, frames=frames))
+    rows = None
+    if frames is not None:
+        rows = torch.tensor([model.get_output_length(f) for f in frames], dtype=torch.int32).to(audio.device)
+    toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False, out=out, frames=rows)
     return toks, lens
 
 

@@ -2,24 +2,24 @@
 
 The reference scripts run one file at a time: load -> mel on the host -> (1, F, 80) forward
 -> greedy decode (reference scripts/transcribe.py:48-131, scripts/evaluate.py:60-107).
-Here files are read on the host, then grouped by sample count and each group goes through
-the device pipeline as one batch (mel, forward, argmax, collapse all on the HIP device).
-Utterances are never padded — the model has no padding masks, so a padded clip would give
-different logits — and every utterance's computation is independent of its batch
-neighbours, so the output for a file is the one the per-file loop produces.
+Here files are read on the host, sorted by length and cut into batches that go through the
+device pipeline together (mel, forward, argmax, collapse all on the HIP device).  A batch of
+clips of different lengths is zero-padded to its longest clip and carries each clip's own
+length (pipeline.audio_to_token_ids(..., lengths=)): the mel statistics, pooling sizes,
+attention keys and the collapse follow each clip's length and the SSM stacks are causal, so
+the output for a file is the one the reference's per-file loop produces.
 """
 
 from __future__ import annotations
 
 import logging
-from collections import OrderedDict
 from pathlib import Path
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import torch
 
 from . import ops
-from .audio import HOP_LENGTH, SAMPLE_RATE, load_audio, mel_on_device
+from .audio import HOP_LENGTH, N_FFT, SAMPLE_RATE, load_audio, mel_on_device
 from .decode import CTCDecoder
 
 logger = logging.getLogger(__name__)
@@ -69,15 +69,24 @@ def group_words(tokens: Sequence[int], spans: Sequence[Tuple[int, int]], vocabul
 
 
 def _decode_batch(model, audio: torch.Tensor, decoder: CTCDecoder, timestamps: bool,
-                  beam_width: int = 1) -> List[Tuple[str, Optional[List[Dict]]]]:
-    """(b, S) device audio -> [(text, words or None)] through the device pipeline."""
+                  beam_width: int = 1, lengths: Optional[List[int]] = None) -> List[Tuple[str, Optional[List[Dict]]]]:
+    """(b, S) device audio -> [(text, words or None)] through the device pipeline.  lengths:
+    per-clip sample counts when the clips were zero-padded to S."""
     with torch.no_grad():
-        mel = mel_on_device(audio, n_mels=model.config.mel_bins)
+        mel = mel_on_device(audio, n_mels=model.config.mel_bins, lengths=lengths)
+        frames = None if lengths is None else [n // HOP_LENGTH + 1 for n in lengths]
         if beam_width > 1:
-            logits = model(mel)
-            return [(t, None) for t in decoder.decode_beam_search(logits, beam_width=beam_width)]
+            logits = model(mel, frames=frames)
+            if frames is None:
+                return [(t, None) for t in decoder.decode_beam_search(logits, beam_width=beam_width)]
+            return [(decoder.decode_beam_search(logits[b:b + 1, :model.get_output_length(f)],
+                                                beam_width=beam_width)[0], None) for b, f in enumerate(frames)]
         # greedy: the CTC head's GEMM reduces each frame to its argmax (no logits in HBM)
-        toks, lens, st, en = ops.ctc_collapse(model.token_ids(mel), decoder.blank_token, True, timestamps)
+        rows = None
+        if frames is not None:
+            rows = torch.tensor([model.get_output_length(f) for f in frames], dtype=torch.int32).to(audio.device)
+        toks, lens, st, en = ops.ctc_collapse(model.token_ids(mel, frames=frames), decoder.blank_token, True,
+                                              timestamps, frames=rows)
     toks, lens = toks.cpu().numpy(), lens.cpu().numpy()
     if timestamps:
         st, en = st.cpu().numpy(), en.cpu().numpy()
@@ -103,30 +112,38 @@ def transcribe_files(model, paths: Iterable, decoder: CTCDecoder, device, timest
     """
     paths = [str(p) for p in paths]
     results: List[Optional[Dict]] = [None] * len(paths)
-    groups: "OrderedDict[int, List[Tuple[int, torch.Tensor]]]" = OrderedDict()
+    items: List[Tuple[int, torch.Tensor]] = []
     for i, p in enumerate(paths):
         try:
             a = load_audio(p)
             if a.dim() != 1 or a.numel() < 2:
                 raise ValueError(f"expected a mono clip of at least 2 samples, got shape {tuple(a.shape)}")
-            groups.setdefault(a.numel(), []).append((i, a))
+            if a.numel() <= N_FFT // 2:  # the reference's reflect padding rejects it too
+                raise RuntimeError(f"compute_mel_spectrogram: reflect padding of {N_FFT // 2} needs more than "
+                                   f"{N_FFT // 2} samples, got {a.numel()}")
+            items.append((i, a))
         except Exception as e:  # reported per file, like the reference's loop
             results[i] = {"file": p, "error": str(e)}
     dev = torch.device(device)
-    for n, items in groups.items():
-        for k in range(0, len(items), max(1, batch_size)):
-            chunk = items[k:k + batch_size]
-            try:
-                audio = torch.stack([a for _, a in chunk]).to(dev, torch.float32)
-                decoded = _decode_batch(model, audio, decoder, timestamps, beam_width)
-                for (i, _), (text, words) in zip(chunk, decoded):
-                    r = {"file": paths[i], "duration": n / SAMPLE_RATE, "transcription": text}
-                    if timestamps:
-                        r["words"] = words
-                    results[i] = r
-            except Exception as e:
-                for i, _ in chunk:
-                    results[i] = {"file": paths[i], "error": str(e)}
+    items.sort(key=lambda it: it[1].numel())  # neighbours of similar length: little padding
+    for k in range(0, len(items), max(1, batch_size)):
+        chunk = items[k:k + batch_size]
+        try:
+            ns = [a.numel() for _, a in chunk]
+            S = max(ns)
+            audio = torch.zeros((len(chunk), S), dtype=torch.float32)
+            for j, (_, a) in enumerate(chunk):
+                audio[j, :ns[j]] = a.to(torch.float32)
+            decoded = _decode_batch(model, audio.to(dev), decoder, timestamps, beam_width,
+                                    lengths=None if min(ns) == S else ns)
+            for (i, _), n, (text, words) in zip(chunk, ns, decoded):
+                r = {"file": paths[i], "duration": n / SAMPLE_RATE, "transcription": text}
+                if timestamps:
+                    r["words"] = words
+                results[i] = r
+        except Exception as e:
+            for i, _ in chunk:
+                results[i] = {"file": paths[i], "error": str(e)}
     return results  # type: ignore[return-value]
 
 
