@@ -31,3 +31,20 @@ def golden_json(name):
 def default_weights():
     from velocity_asr import synthetic
     return synthetic.make_weights(None, seed=0)
+
+
+def record_error(got, want, tol):
+    """Append {test, max_abs, worst |diff| / (atol + rtol |want|)} to $VASR_PARITY_LOG (JSON lines)
+    when it is set: the measured margin of a float comparison, reported in DESIGN.md §4."""
+    path = os.environ.get("VASR_PARITY_LOG")
+    if not path:
+        return
+    got = np.asarray(got, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)
+    d = np.abs(got - want)
+    rec = dict(test=os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0],
+               max_abs=float(d.max()) if d.size else 0.0,
+               max_rel=float((d / np.maximum(np.abs(want), 1e-30)).max()) if d.size else 0.0,
+               tol_use=float((d / (tol["atol"] + tol["rtol"] * np.abs(want))).max()) if d.size else 0.0)
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")

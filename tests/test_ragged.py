@@ -13,13 +13,13 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import golden, record_error
 from oracle import velocity_ref as R
 from velocity_asr import synthetic as S
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-LOGIT_TOL = dict(atol=5e-4, rtol=1e-4)
+LOGIT_TOL = dict(atol=1e-4, rtol=1e-5)  # SURVEY §8(d); measured max |diff| 8.2e-6
 
 
 @pytest.fixture(scope="module")
@@ -108,6 +108,7 @@ def test_padded_batch_logits_vs_oracle(va, model):
     for b, c in enumerate(clips):
         ref = R.forward(W, R.compute_mel_spectrogram(c[None]), dict(S.DEFAULT_CONFIG))
         L = ref.shape[1]
+        record_error(logits[b:b + 1, :L], ref, LOGIT_TOL)
         np.testing.assert_allclose(logits[b:b + 1, :L], ref, **LOGIT_TOL, err_msg=f"clip {b}")
         np.testing.assert_array_equal(logits[b, :L].argmax(-1), ref[0].argmax(-1))
     same = _pad([c[:4000] for c in clips])[0]

@@ -5,7 +5,7 @@ Mode 2 evaluates the same exclusive, mis-combined Blelloch tree as the reference
 _associative_scan (ssm.py:216-295) but rounds each a*b + c once (v_pk_fma_f32) and forms
 x*dt before scaling B (ssm.py:198-202 form x*(dt*B)), so it is no longer op-for-op equal
 to the reference; the bar is the fp32 one of the whole suite:
-  * logits vs reference golden: atol 5e-4, rtol 1e-4
+  * logits vs reference golden: atol 1e-4, rtol 1e-5 (measured max 8.2e-6)
   * CTC argmax tokens and greedy token lists: bit-exact
 """
 
@@ -13,13 +13,13 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, golden_json
+from conftest import golden, golden_json, record_error
 from velocity_asr import synthetic as S
 
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-LOGIT_TOL = dict(atol=5e-4, rtol=1e-4)
+LOGIT_TOL = dict(atol=1e-4, rtol=1e-5)  # SURVEY §8(d); measured max |diff| 8.2e-6
 
 
 @pytest.fixture(scope="module")
@@ -53,6 +53,7 @@ def test_fma_headline_shape_b2_10s(va, model, fma):
     g = golden("fwd_b2_10s.npz")
     logits = model(va.compute_mel_spectrogram(t(S.make_audio(2, 160000, seed=1234))))
     np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
+    record_error(logits[:, g["frames"]].cpu().numpy(), g["logits_sub"], LOGIT_TOL)
     np.testing.assert_allclose(logits[:, g["frames"]].cpu().numpy(), g["logits_sub"], **LOGIT_TOL)
     assert va.ctc_greedy_decode(logits) == golden_json("decode_fwd.json")["results"]["b2_10s"]
 
@@ -61,6 +62,7 @@ def test_fma_b2_3s_and_stages(va, model, fma):
     g = golden("fwd_b2_3s.npz")
     logits, f = model(t(g["mel"]), return_features=True)
     np.testing.assert_allclose(f["local_features"].cpu().numpy(), g["local_features"], atol=3e-4, rtol=1e-4)
+    record_error(logits.cpu().numpy(), g["logits"], LOGIT_TOL)
     np.testing.assert_allclose(logits.cpu().numpy(), g["logits"], **LOGIT_TOL)
     np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
 
@@ -69,6 +71,7 @@ def test_fma_long_utterance_30s(va, model, fma):
     g = golden("fwd_b1_30s.npz")
     logits = model(va.compute_mel_spectrogram(t(S.make_audio(1, 480000, seed=4321))))
     np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
+    record_error(logits[:, g["frames"]].cpu().numpy(), g["logits_sub"], LOGIT_TOL)
     np.testing.assert_allclose(logits[:, g["frames"]].cpu().numpy(), g["logits_sub"], **LOGIT_TOL)
 
 
@@ -76,10 +79,12 @@ def test_fma_edge_lengths_and_chirp(va, model, fma):
     g = golden("fwd_edge.npz")
     for S_, seed in ((201, 31), (400, 32), (1600, 33), (8000, 34), (16333, 35)):
         logits = model(va.compute_mel_spectrogram(t(S.make_audio(1, S_, seed=seed))))
+        record_error(logits.cpu().numpy(), g[f"S{S_}__logits"], LOGIT_TOL)
         np.testing.assert_allclose(logits.cpu().numpy(), g[f"S{S_}__logits"], **LOGIT_TOL)
         np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g[f"S{S_}__tokens"])
     g = golden("fwd_chirp_3s.npz")
     logits = model(va.compute_mel_spectrogram(t(S.make_chirp(48000)[None])))
+    record_error(logits.cpu().numpy(), g["logits"], LOGIT_TOL)
     np.testing.assert_allclose(logits.cpu().numpy(), g["logits"], **LOGIT_TOL)
     np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
 
