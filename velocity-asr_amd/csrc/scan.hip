@@ -232,11 +232,14 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
                    "vasr_ssm_scan_f32: inputs must be 16-byte aligned");
     if (B == 0 || L == 0) return VASR_OK;
     hipStream_t s = as_stream(stream);
-    // Lane layout (B * Di * N / 256 waves at 4 state indices per lane).  2 per lane halves each
-    // wave's serial chain but costs ~35 % more VALU per element: faster only when the launch is
-    // latency-bound with under half a wave per SIMD (B <= 4 at Di 384, N 64: 62 vs 69 us), and
-    // at the bench's 16-clip launches the extra issue slots slow the concurrent stream's GEMMs
-    // (97.5k vs 102.5k RTFx end to end).  VASR_SCAN_NPL=2|4 forces one.
+    // Lane layout (B * Di * N / 256 waves at 4 state indices per lane).  A lone wave issues a
+    // VALU instruction every ~8.5 cycles; two or more per SIMD reach the SIMD's rate.  2 per lane
+    // (twice the waves, ~25 % more VALU per element) is faster ALONE below 2 waves per SIMD: the
+    // bench's 16-clip launch 76 vs 81 us, 79 vs 86 us in the graph (32 clips: 134 vs 114 us).
+    // But its extra VALU issue slows the other utterance group's concurrent GEMMs: end to end
+    // C2 +1.3 %, C3 (bf16) -2.6 %, C4 (30 s) -8.5 % (profiles/r02_npl/).  So 2 per lane is kept
+    // for launches under half a wave per SIMD (B <= 4 at Di 384, N 64: 62 vs 69 us), where the
+    // shorter serial chain per wave wins.  VASR_SCAN_NPL=2|4 forces one.
     const char* npl_s = std::getenv("VASR_SCAN_NPL");  // read per call (tests switch it)
     const int npl_env = npl_s ? std::atoi(npl_s) : 0;
     const long waves4 = (long)B * Di * N / 256;
