@@ -2,8 +2,10 @@
 
 Only one GPU is available to the tests, so the RCCL path runs at world size 1 in a child
 process (scatter from rank 0, HIP graphs, gather), and bench.py's launcher is exercised end
-to end with --gpus 1 (torch.distributed.run as a child, one rank).  Larger worlds are covered
-by the gloo tests in tests/test_distributed.py and by the driver's 8-GPU scaling run."""
+to end with --gpus 1 (torch.distributed.run as a child, one rank).  The sharded form at world
+size 2 (C3's partitioning: rank r transcribes its own slice of the batch) runs with both ranks
+on the one GPU over a gloo group (RCCL refuses two ranks on one device): real HIP steps,
+host-side scatter/gather.  The 8-GPU RCCL run is the driver's scaling bench."""
 
 import json
 import os
@@ -90,3 +92,66 @@ def test_bench_launcher_one_gpu():
     assert d["with_scatter"]["rank0_tokens_match"] is True and d["with_scatter"]["value"] > 0
     for k in ("valu_frac", "hbm_ceiling_frac", "gemm_frac", "gemm_f32eq_frac"):
         assert k in d["roofline"], k
+
+
+CHILD2 = r"""
+import json, os, sys
+sys.path[:0] = [{pkg!r}, {repo!r}]
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+dev = torch.device("cuda", 0)  # both ranks share the one GPU
+torch.cuda.set_device(dev)
+import velocity_asr as va
+from velocity_asr import synthetic as S
+from velocity_asr.distributed import hip_step, shard_range, transcribe_sharded
+from velocity_asr.pipeline import audio_to_token_ids, token_lists
+res = {{}}
+for dtype in ("f32", "bf16"):
+    m = va.VELOCITYASR()
+    m.load_state_dict({{k: torch.from_numpy(v) for k, v in S.make_weights(None, seed=0).items()}}, strict=True)
+    m = m.to(dev).eval()
+    if dtype == "bf16":
+        m = m.to(torch.bfloat16)  # BASELINE C3: the bf16 model, 32 clips per GPU
+    step = hip_step(m)
+
+    def host_step(shard):  # gloo moves host tensors: shard to the GPU, tokens back
+        t, n = step(shard.to(dev))
+        return t.cpu(), n.cpu()
+
+    audio = torch.from_numpy(S.make_audio(4, 160000, seed=1234)) if rank == 0 else None
+    lists = transcribe_sharded(host_step, audio, 4, 160000, torch.device("cpu"))
+    if rank == 0:
+        # the same 4 clips in one unsharded batch on this process
+        whole = token_lists(*audio_to_token_ids(m, audio.to(dev)))
+        res[dtype] = dict(sharded=lists, whole=whole)
+    lo, hi = shard_range(4, world, rank)
+    res.setdefault("ranges", {{}})[dtype] = [lo, hi]
+if rank == 0:
+    print("RESULT " + json.dumps(res), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_two_rank_sharded_transcription_one_gpu(tmp_path):
+    """World size 2 with both ranks on the one GPU (gloo transport): each rank runs the real
+    HIP step on its half of the batch; rank 0's gathered token lists equal the reference's for
+    the fp32 model (the bench's first 4 clips, tests/golden/fwd_fullbatch.npz) and, for the
+    bf16 model (C3), the unsharded batch on the same device."""
+    from conftest import golden
+    script = tmp_path / "child2.py"
+    script.write_text(CHILD2.format(pkg=PKG_ROOT, repo=REPO))
+    env = _env()
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", env["MASTER_PORT"], str(script)],
+                       env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    res = json.loads(line[len("RESULT "):])
+    exp = json.loads(str(golden("fwd_fullbatch.npz")["greedy"]))["c2"][:4]
+    assert res["f32"]["sharded"] == exp
+    assert res["f32"]["whole"] == exp
+    assert res["bf16"]["sharded"] == res["bf16"]["whole"]
+    assert res["ranges"]["f32"] == [0, 2]
