@@ -62,6 +62,21 @@ def test_tail_matches_fp64(M):
     np.testing.assert_allclose(got, ref, atol=2e-5 * max(1.0, np.abs(ref).max()), rtol=2e-5)
 
 
+@pytest.mark.parametrize("M", [17, 501, 4097])
+def test_tail_row_forms_bitwise_equal(monkeypatch, M):
+    """16- and 32-row workgroups (VASR_TAIL_ROWS; the default takes 16 up to M = 4096) perform the
+    same float operations per element: outputs are bitwise equal."""
+    rng = np.random.default_rng(M + 1)
+    P = _params(9)
+    g = rng.standard_normal((M, 384)).astype(np.float32)
+    x = rng.standard_normal((M, 192)).astype(np.float32)
+    monkeypatch.setenv("VASR_TAIL_ROWS", "16")
+    a = _run(g, x, P)
+    monkeypatch.setenv("VASR_TAIL_ROWS", "32")
+    b = _run(g, x, P)
+    np.testing.assert_array_equal(a, b)
+
+
 def test_tail_strided_input():
     rng = np.random.default_rng(3)
     P = _params(8)

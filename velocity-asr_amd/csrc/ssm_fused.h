@@ -80,10 +80,11 @@ __device__ __forceinline__ floatx4 mac_tile(const bf16x8 (&a)[NP], const bf16x8 
 }
 
 // the A fragment of one 16-row tile for a 32-k step: NP chunks of the plane image at `base`
-template <int NP, int WIDTH>
+// (planes of ROWS rows)
+template <int NP, int WIDTH, int ROWS = TBM>
 __device__ __forceinline__ void read_a(const char* base, int row, int ks, int q, bf16x8 (&a)[NP]) {
     constexpr int SW = WIDTH == TE ? 15 : 7;
-    constexpr int PB = TBM * WIDTH * 2;
+    constexpr int PB = ROWS * WIDTH * 2;
 #pragma unroll
     for (int pl = 0; pl < NP; ++pl)
         a[pl] = *reinterpret_cast<const bf16x8*>(base + pl * PB + row * WIDTH * 2 + (((4 * ks + q) ^ (row & SW)) << 4));

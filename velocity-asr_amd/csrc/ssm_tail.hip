@@ -19,7 +19,8 @@
 // result is an fp32 computation of the block tail; it differs from the unfused launches only
 // in the MFMA accumulation grouping (32 k per instruction here, 16 there).
 //
-// Work decomposition: 4 waves (one per SIMD), 32 token rows; each output 32 x 192 is 2 x 12
+// Work decomposition: 4 waves (one per SIMD), 32 token rows (16 for small launches, see
+// tail_rows); each output 32 x 192 is 2 x 12
 // tiles of 16 x 16 and wave w owns column tiles 3w .. 3w + 2 of both row tiles (FFN1's 32 x 384
 // runs as two 192-column halves with the same map), so no two waves need the same weight
 // fragment: weights go global -> VGPRs straight from their fragment-native split planes, each
@@ -29,6 +30,8 @@
 // of row r at c ^ (r & 15) (384-wide) or c ^ (r & 7) (192-wide): conflict-free fragment reads.
 // LDS: 72 KiB for the 384-wide planes (g, then f; the fp32 x1 scratch of the LayerNorm lives
 // there in between) + 36 KiB for the 192-wide planes of h.
+#include <cstdlib>
+
 #include "ssm_fused.h"
 
 namespace vasr {
@@ -43,8 +46,11 @@ constexpr int NSTAGES = 36;      // out_proj 12 k-steps, FFN1 2 halves x 6, FFN2
 #ifndef VASR_TAIL_PD
 #define VASR_TAIL_PD 3
 #endif
-template <int NP>
-constexpr int pd_of() { return NP == 3 ? VASR_TAIL_PD : 6; }
+#ifndef VASR_TAIL_PD16
+#define VASR_TAIL_PD16 2  // the 16-row form (two waves per SIMD: 256 registers, no spills at 2)
+#endif
+template <int NP, int RT = 2>
+constexpr int pd_of() { return NP == 3 ? (RT == 1 ? VASR_TAIL_PD16 : VASR_TAIL_PD) : 6; }
 
 struct TailParams {
     const float* g;
@@ -64,24 +70,29 @@ struct TailParams {
     int M;
 };
 
-template <int NP>
+// RT = 16-row tiles per workgroup: 2 (32 rows, one block per CU) or 1 (16 rows, half the LDS,
+// two blocks per CU: twice the weight stream per row, two waves per SIMD to hide it)
+template <int NP, int RT>
 struct TailCtx {
-    static constexpr int PD = pd_of<NP>();
+    static constexpr int PD = pd_of<NP, RT>();
     static constexpr int RING = PD + 1;
+    static constexpr int ROWS = 16 * RT;
+    static constexpr int PE = ROWS * TE * 2;  // one bf16 plane of a 384-wide A tile
+    static constexpr int PDB = ROWS * TD * 2;  // one bf16 plane of a 192-wide A tile
     const TailParams& P;
     char* R;   // 384-wide planes (g, f) / fp32 x1 scratch
     char* H;   // 192-wide planes (h)
     int lane, wave, r, q, m0;
-    floatx4 acc[2][3];
+    floatx4 acc[RT][3];
     bf16x8 w[RING][3][NP];  // [ring slot][column tile][plane]
-    float x1[2][3][4];     // residual x, then x1 = out_proj(g) + x
+    float x1[RT][3][4];     // residual x, then x1 = out_proj(g) + x
     float bb1[2][3], bb2[3], lnw[3], lnb[3];
 };
 
 // weight fragments of step S for this wave: column tiles 3w .. 3w+2, NP planes, from the
 // fragment layout [N/16][K/32][NP][64][8]
-template <int S, int NP>
-__device__ __forceinline__ void load_w(TailCtx<NP>& c) {
+template <int S, int NP, int RT>
+__device__ __forceinline__ void load_w(TailCtx<NP, RT>& c) {
     const uint16_t* W;
     int nt0, ks, KS;
     if constexpr (S < 12) {
@@ -96,39 +107,40 @@ __device__ __forceinline__ void load_w(TailCtx<NP>& c) {
         const int nt = nt0 + 3 * c.wave + t;
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl)
-            c.w[S % TailCtx<NP>::RING][t][pl] =
+            c.w[S % TailCtx<NP, RT>::RING][t][pl] =
                 *reinterpret_cast<const bf16x8*>(W + ((int64_t)(nt * KS + ks) * NP + pl) * 512 + c.lane * 8);
     }
 }
 
 // the first PD steps' weights (prologue)
-template <int S, int NP>
-__device__ __forceinline__ void load_first(TailCtx<NP>& c) {
-    load_w<S, NP>(c);
-    if constexpr (S + 1 < TailCtx<NP>::PD) load_first<S + 1, NP>(c);
+template <int S, int NP, int RT>
+__device__ __forceinline__ void load_first(TailCtx<NP, RT>& c) {
+    load_w<S, NP, RT>(c);
+    if constexpr (S + 1 < TailCtx<NP, RT>::PD) load_first<S + 1, NP, RT>(c);
 }
 
-template <int S, int NP>
-__device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
-    constexpr int PD = TailCtx<NP>::PD;
-    if constexpr (S + PD < NSTAGES) load_w<S + PD, NP>(c);
+template <int S, int NP, int RT>
+__device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
+    using Ctx = TailCtx<NP, RT>;
+    constexpr int PD = Ctx::PD;
+    if constexpr (S + PD < NSTAGES) load_w<S + PD, NP, RT>(c);
     // keep the prefetch where it is: without this fence the scheduler sinks the loads next to
     // their use (to save registers) and the step then waits on them (measured: the weight
     // stream then ran at a third of the L2 rate)
     __builtin_amdgcn_sched_barrier(0);
     // A fragments of both row tiles
-    bf16x8 a[2][NP];
+    bf16x8 a[RT][NP];
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm) {
+    for (int tm = 0; tm < RT; ++tm) {
         if constexpr (S < 12 || S >= 24)
-            read_a<NP, TE>(c.R, 16 * tm + c.r, S < 12 ? S : S - 24, c.q, a[tm]);
+            read_a<NP, TE, Ctx::ROWS>(c.R, 16 * tm + c.r, S < 12 ? S : S - 24, c.q, a[tm]);
         else
-            read_a<NP, TD>(c.H, 16 * tm + c.r, (S - 12) % 6, c.q, a[tm]);
+            read_a<NP, TD, Ctx::ROWS>(c.H, 16 * tm + c.r, (S - 12) % 6, c.q, a[tm]);
     }
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % TailCtx<NP>::RING][t], c.acc[tm][t]);
+        for (int t = 0; t < 3; ++t) c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % Ctx::RING][t], c.acc[tm][t]);
 
     if constexpr (S == 11) {
         // x1 = out_proj(g) + x (registers, kept for the final residual) -> fp32 scratch in R
@@ -136,7 +148,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
         lds_barrier();
         float* xs = reinterpret_cast<float*>(c.R);
 #pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
+        for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
             for (int t = 0; t < 3; ++t) {
                 const int col = 16 * (3 * c.wave + t) + c.r;
@@ -151,8 +163,8 @@ __device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
         // h = LayerNorm_2(x1): one wave per row with vasr_layer_norm_f32's operations, each
         // value split into the three planes of H
 #pragma unroll
-        for (int k = 0; k < TBM / TWAVES; ++k) {
-            const int rr = TBM / TWAVES * c.wave + k;
+        for (int k = 0; k < Ctx::ROWS / TWAVES; ++k) {
+            const int rr = Ctx::ROWS / TWAVES * c.wave + k;
             float v[3];
             float sum = 0.f;
 #pragma unroll
@@ -171,43 +183,44 @@ __device__ __forceinline__ void tail_step(TailCtx<NP>& c) {
             const float rstd = 1.0f / sqrtf(var + c.P.ln_eps);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
-                split_store<NP>(c.H, PLANE_D, poff<TD>(rr, c.lane + 64 * i), __builtin_fmaf((v[i] - mean) * rstd, c.lnw[i], c.lnb[i]));
+                split_store<NP>(c.H, Ctx::PDB, poff<TD>(rr, c.lane + 64 * i), __builtin_fmaf((v[i] - mean) * rstd, c.lnw[i], c.lnb[i]));
         }
         lds_barrier();  // h complete; the scratch in R is free for f
     } else if constexpr (S == 17 || S == 23) {
         // f = GELU(ffn.0(h) + b1), FFN1 column half hh, split into the planes of R
         constexpr int hh = S == 17 ? 0 : 1;
 #pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
+        for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
             for (int t = 0; t < 3; ++t) {
                 const int col = TD * hh + 16 * (3 * c.wave + t) + c.r;
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    split_store<NP>(c.R, PLANE_E, poff<TE>(16 * tm + 4 * c.q + i, col),
+                    split_store<NP>(c.R, Ctx::PE, poff<TE>(16 * tm + 4 * c.q + i, col),
                                 gelu_fast(c.acc[tm][t][i] + c.bb1[hh][t]));
                 c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         if constexpr (S == 23) lds_barrier();  // f complete before FFN2 reads it
     }
-    if constexpr (S + 1 < NSTAGES) tail_step<S + 1, NP>(c);
+    if constexpr (S + 1 < NSTAGES) tail_step<S + 1, NP, RT>(c);
 }
 
-template <int NP>
-__global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
-    __shared__ __attribute__((aligned(16))) char R[NP * PLANE_E];
-    __shared__ __attribute__((aligned(16))) char H[NP * PLANE_D];
-    TailCtx<NP> c{P, R, H};
+template <int NP, int RT>
+__global__ __launch_bounds__(256, RT == 1 ? 2 : 1) void ssm_tail_kernel(TailParams P) {
+    using Ctx = TailCtx<NP, RT>;
+    __shared__ __attribute__((aligned(16))) char R[NP * Ctx::PE];
+    __shared__ __attribute__((aligned(16))) char H[NP * Ctx::PDB];
+    Ctx c{P, R, H};
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     c.r = c.lane & 15;
     c.q = c.lane >> 4;
-    c.m0 = blockIdx.x * TBM;
+    c.m0 = blockIdx.x * Ctx::ROWS;
     // weights of the first PD steps, then the g tile (split once into R's planes), the residual
     // x and the epilogue constants: all of these loads are in flight together
-    load_first<0, NP>(c);
+    load_first<0, NP, RT>(c);
     __builtin_amdgcn_sched_barrier(0);
-    constexpr int UNITS = TBM * TE / 8;  // 8-float chunks of the g tile
+    constexpr int UNITS = Ctx::ROWS * TE / 8;  // 8-float chunks of the g tile
 #pragma unroll
     for (int k = 0; k < UNITS / 256; ++k) {
         const int u = threadIdx.x + 256 * k;
@@ -215,10 +228,10 @@ __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
         const float* src = P.g + (int64_t)min(c.m0 + rr, P.M - 1) * P.ldg + 8 * ch;
         const float4 v0 = *reinterpret_cast<const float4*>(src);
         const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
-        split_store8<NP>(R, PLANE_E, rr * TE * 2 + ((ch ^ (rr & 15)) << 4), v0, v1);
+        split_store8<NP>(R, Ctx::PE, rr * TE * 2 + ((ch ^ (rr & 15)) << 4), v0, v1);
     }
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const int col = 16 * (3 * c.wave + t) + c.r;
@@ -238,10 +251,10 @@ __global__ __launch_bounds__(256, 1) void ssm_tail_kernel(TailParams P) {
         c.lnb[i] = P.ln_b[c.lane + 64 * i];
     }
     lds_barrier();  // the g planes are complete
-    tail_step<0, NP>(c);
+    tail_step<0, NP, RT>(c);
     // out = ffn.3(f) + b2 + x1
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
             const int col = 16 * (3 * c.wave + t) + c.r;
@@ -296,6 +309,17 @@ __global__ void pack_weights16_kernel(const uint16_t* __restrict__ W, int64_t ld
     for (int j = 0; j < 8; ++j) dst[j] = (n < N && k0 + j < K) ? W[(int64_t)n * ldw + k0 + j] : (uint16_t)0;
 }
 
+// Rows per workgroup.  A block's time is set by its own weight stream and MFMA chain (23 us at
+// 32 rows whatever M is, 21 us at 16), so 16-row blocks win while they still fit one per CU
+// (M <= 4096: the global-context blocks, one utterance at a time); above that two 16-row blocks
+// per CU duplicate the per-CU L2 -> VGPR weight stream: 33.2 vs 28.3 us at M = 8016,
+// 135.5k vs 136.1k RTFx end to end (profiles/r02e/tail_rows.txt).  VASR_TAIL_ROWS=16|32 forces
+// one (read per call).
+int tail_rows(int M) {
+    if (const char* e = std::getenv("VASR_TAIL_ROWS")) return std::atoi(e) == 16 ? 16 : 32;
+    return M <= 4096 ? 16 : 32;  // 256 CUs x 16 rows
+}
+
 int tail_args(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo, const float* ln_w,
               const float* ln_b, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2, float* out,
               int64_t ldo, int M, int D, int E, const char* fn) {
@@ -340,7 +364,10 @@ VASR_API int vasr_ssm_block_tail_bf16(const float* g, int64_t ldg, const float* 
         return rc;
     if (M == 0) return VASR_OK;
     TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
-    hipLaunchKernelGGL(ssm_tail_kernel<1>, dim3((M + TBM - 1) / TBM), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    if (tail_rows(M) == 16)
+        hipLaunchKernelGGL((ssm_tail_kernel<1, 1>), dim3((M + 15) / 16), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    else
+        hipLaunchKernelGGL((ssm_tail_kernel<1, 2>), dim3((M + 31) / 32), dim3(64 * TWAVES), 0, as_stream(stream), p);
     return launch_status("vasr_ssm_block_tail_bf16");
 }
 
@@ -371,6 +398,9 @@ VASR_API int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x
         return rc;
     if (M == 0) return VASR_OK;
     TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
-    hipLaunchKernelGGL(ssm_tail_kernel<3>, dim3((M + TBM - 1) / TBM), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    if (tail_rows(M) == 16)
+        hipLaunchKernelGGL((ssm_tail_kernel<3, 1>), dim3((M + 15) / 16), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    else
+        hipLaunchKernelGGL((ssm_tail_kernel<3, 2>), dim3((M + 31) / 32), dim3(64 * TWAVES), 0, as_stream(stream), p);
     return launch_status("vasr_ssm_block_tail_f32");
 }
