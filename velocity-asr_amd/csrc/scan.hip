@@ -26,7 +26,8 @@
 // are staged to LDS (double-buffered, register prefetch of the next chunk); the four
 // in-chunk stack levels are compile-time registers (step i's push/merge pattern is a
 // constant, full chunks carry no per-step guards); chunk-sized blocks form the upper stack,
-// merged once per chunk.  Blocks are remapped so all channel blocks of one utterance share
+// merged once per chunk.  Launches of at most two waves per SIMD run 32-step chunks (five
+// in-chunk levels; see launch_n).  Blocks are remapped so all channel blocks of one utterance share
 // an XCD (its 4 MiB L2 then serves the B/C slices and the 64-B row segments they share).
 #include <cstdlib>
 
@@ -46,6 +47,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 #endif
 #ifndef VASR_SCAN_WAVES_NPL2
 #define VASR_SCAN_WAVES_NPL2 4  // the same for the 2-states-per-lane layout
+#endif
+#ifndef VASR_SCAN_WAVES_TC32
+#define VASR_SCAN_WAVES_TC32 2  // the 32-step-chunk kernel (VASR_SCAN_T=32): one more stack level
 #endif
 #ifndef VASR_SCAN_FASTSTAGE
 #define VASR_SCAN_FASTSTAGE 1  // 0: every chunk's staging addresses from the clamped index path
@@ -68,7 +72,7 @@ __device__ __forceinline__ f2 operator+(f2 a, f2 b) { return f2{a.x + b.x, a.y +
 #endif
 
 constexpr float LOG2E_F = 1.4426950408889634f;
-constexpr int T = 16;    // time steps per chunk
+constexpr int T = 16;    // time steps per chunk (the chunk-parallel form; the streaming kernel's TC)
 constexpr int TP = T + 1;  // padded row of the per-channel partial-sum tile
 constexpr int NW = 4;    // waves per block
 
@@ -76,9 +80,10 @@ constexpr int ctz_c(int v) { return v & 1 ? 0 : 1 + ctz_c(v >> 1); }
 constexpr int trailing_ones(int v) { return v & 1 ? 1 + trailing_ones(v >> 1) : 0; }
 // Level of the stack entry right below a new block at level j after step i (count i+1),
 // or -1 when the entry below is the upper (chunk-level) stack.
-constexpr int below_level(int i, int j) {
+// lg = in-chunk stack levels (log2 of the chunk length).
+constexpr int below_level(int i, int j, int lg = 4) {
     return ((i + 1) >> (j + 1)) == 0 ? -1
-           : (j + 1 + ctz_c((i + 1) >> (j + 1)) < 4 ? j + 1 + ctz_c((i + 1) >> (j + 1)) : -1);
+           : (j + 1 + ctz_c((i + 1) >> (j + 1)) < lg ? j + 1 + ctz_c((i + 1) >> (j + 1)) : -1);
 }
 
 template <int CTRL>
@@ -166,15 +171,15 @@ __device__ __forceinline__ void reduce_half(float (&v)[8], int g) {
 }
 
 // Reduce the partial sums of steps [8*HALF, 8*HALF + 8) and store them to the channel's row
-// of the partial-sum tile ([DPB][TP] floats).
-template <int G, int HALF>
-__device__ __forceinline__ void flush_half(float (&yv)[T], float* yp, int dl, int g) {
+// of the partial-sum tile ([DPB][TC + 1] floats; TC = chunk length).
+template <int G, int HALF, int TC = T>
+__device__ __forceinline__ void flush_half(float (&yv)[TC], float* yp, int dl, int g) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = yv[HALF * 8 + j];
     reduce_half<G>(v, g);
 #pragma unroll
-    for (int j = 0; j < HalfReduce<G>::SF; ++j) yp[dl * TP + HALF * 8 + HalfReduce<G>::step(j, g)] = v[j];
+    for (int j = 0; j < HalfReduce<G>::SF; ++j) yp[dl * (TC + 1) + HALF * 8 + HalfReduce<G>::step(j, g)] = v[j];
 }
 
 // a * b + c: two roundings as in the reference tree (modes 0), or one fused multiply-add
