@@ -76,7 +76,8 @@ def main(tag):
                      f"{'' if wr is None else f'{wr / 1e6:.1f}'} |")
         fam = family(r["Name"])
         if fam in ("ssm_scan",) and rd is not None:
-            traffic[fam] = {str(g): int(v[0] + v[1]) for _, g, v in cands}  # grid size -> bytes
+            # grid size -> bytes, merged over the family's instantiations (chunk lengths, layouts)
+            traffic.setdefault(fam, {}).update({str(g): int(v[0] + v[1]) for _, g, v in cands})
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
