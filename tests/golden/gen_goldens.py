@@ -483,6 +483,55 @@ def gen_fullbatch():
     save("fwd_fullbatch.npz", **out)
 
 
+def _greedy_pack(prefix, model, audio, chunk, out, decoded, cast=None):
+    """Like _tokens_pack for a model whose forward takes `cast(mel)` (bf16): argmax tokens and
+    greedy lists only (margins are meaningless for the statistical configs)."""
+    toks, greedy = [], []
+    for i in range(0, audio.shape[0], chunk):
+        with torch.no_grad():
+            mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(audio[i:i + chunk]))
+            logits = model(cast(mel) if cast else mel).float()
+        toks.append(logits.argmax(-1).numpy().astype(np.int16))
+        greedy.extend(ref_decode.ctc_greedy_decode(logits))
+        print(f"  {prefix}: clips {i}..{i + chunk - 1} done", flush=True)
+    out[prefix + "tokens"] = np.concatenate(toks)
+    decoded[prefix.rstrip("_")] = greedy
+
+
+def gen_benchsets():
+    """The bench's per-rank workloads for every BASELINE config:
+    rank r of `bench.py --gpus N` transcribes make_audio(32, 160000, seed=1234 + r).
+      fp32 (C2 at N > 1): ranks 1..7 (rank 0 is fwd_fullbatch.npz's c2), chunks of 8;
+      bf16 (C3 = 256 clips over 8 ranks): ranks 0..7 with model.to(bfloat16), chunks of 8;
+      int8 (C5): rank 0 with the intended-semantics QAT model calibrated as bench.py does
+      (make_audio(2, 48000, seed=71)).
+    Chunked runs: the reference CPU path is batch-invariant to ~2e-6 (SURVEY §8 e)."""
+    which = os.environ.get("VASR_BENCHSETS", "fp32,bf16,int8").split(",")
+    path = os.path.join(HERE, "fwd_benchsets.npz")
+    out, decoded = {}, {}
+    if os.path.exists(path):  # incremental: keep what an earlier run wrote
+        old = np.load(path, allow_pickle=False)
+        out = {k: old[k] for k in old.files if k not in ("greedy", "meta")}
+        decoded = json.loads(str(old["greedy"]))
+    if "fp32" in which:
+        model = build_model()
+        for r in range(1, 8):
+            _tokens_pack(f"fp32_r{r}_", model, syn.make_audio(32, 160000, seed=1234 + r), 8, out, decoded)
+    if "bf16" in which:
+        model = build_model().to(torch.bfloat16)
+        for r in range(8):
+            _greedy_pack(f"bf16_r{r}_", model, syn.make_audio(32, 160000, seed=1234 + r), 8, out, decoded,
+                         cast=lambda m: m.to(torch.bfloat16))
+    if "int8" in which:
+        qmodel, _ = qat_model(syn.make_audio(2, 48000, seed=71))
+        _greedy_pack("int8_r0_", qmodel, syn.make_audio(32, 160000, seed=1234), 8, out, decoded)
+    out["greedy"] = np.array(json.dumps(decoded))
+    out["meta"] = meta(audio="rank r: make_audio(32, 160000, seed=1234 + r)", weights="make_weights(None, seed=0)",
+                       fp32="ranks 1..7, chunks of 8", bf16="model.to(bfloat16), mel cast to bf16, ranks 0..7",
+                       int8="gen_goldens.qat_model(make_audio(2, 48000, seed=71)), rank 0")
+    save("fwd_benchsets.npz", **out)
+
+
 # --------------------------------------------------------------------------- CLI output
 CLI_CLIPS = {"clip_2s.wav": ("make_audio(1, 32000, seed=91)[0]", lambda: syn.make_audio(1, 32000, seed=91)[0]),
              "chirp_3s.wav": ("make_chirp(48000)", lambda: syn.make_chirp(48000)),
@@ -533,5 +582,7 @@ if __name__ == "__main__":
         gen_beam()
     if "fullbatch" in which:
         gen_fullbatch()
+    if "benchsets" in which:  # long (~30 min on 8 threads): not in the default list
+        gen_benchsets()
     if "cli" in which:
         gen_cli()

@@ -170,3 +170,41 @@ def test_transcribe_script_matches_reference_cli_output(ckpt_and_clips, tmp_path
         got = json.loads(capsys.readouterr().out)
         exp = dict(g[key], file=str(path))
         assert got == exp, key
+
+
+def test_batches_group_equal_lengths_without_ragged_front_end():
+    """without per-length kernels (VASR_STFT=gemm, n_mels > 85) a batch holds clips of
+    one sample count; with them, up to batch_size clips of any length."""
+    from velocity_asr.transcription import _batches
+    items = [(i, torch.zeros(n)) for i, n in enumerate([500, 500, 500, 800, 900, 900, 900, 900, 1200])]
+    lens = lambda bs: [[it[1].numel() for it in b] for b in bs]  # noqa: E731
+    assert lens(_batches(items, 3, True)) == [[500, 500, 500], [800, 900, 900], [900, 900, 1200]]
+    assert lens(_batches(items, 3, False)) == [[500, 500, 500], [800], [900, 900, 900], [900], [1200]]
+    assert lens(_batches(items, 16, False)) == [[500, 500, 500], [800], [900, 900, 900, 900], [1200]]
+    assert list(_batches([], 4, False)) == []
+
+
+@pytest.mark.gpu
+def test_transcribe_files_mixed_lengths_128_mels(tmp_path):
+    """a model with mel_bins = 128 (no per-length front end) over files of different
+    lengths: no file errors, and every file's text equals its transcription alone."""
+    import velocity_asr as v
+    from velocity_asr.audio import write_wav
+    from velocity_asr.transcription import transcribe_files
+    cfg = dict(mel_bins=128, d_model=96, ssm_layers=2, ssm_state_dim=32, global_ssm_state_dim=16,
+               attention_heads=2, attention_dim=24, vocab_size=50)
+    W = S.make_weights(cfg, seed=5)
+    m = v.VELOCITYASR(v.VelocityASRConfig(**cfg))
+    m.load_state_dict({k: torch.from_numpy(w) for k, w in W.items()}, strict=True)
+    m = m.to("cuda").eval()
+    dec = v.CTCDecoder(v.create_default_vocabulary(50))
+    paths = []
+    for i, n in enumerate([16000, 24000, 16000, 9000, 24000]):
+        p = tmp_path / f"c{i}.wav"
+        write_wav(str(p), torch.from_numpy(S.make_audio(1, n, seed=40 + i)[0]), 16000)
+        paths.append(p)
+    got = transcribe_files(m, paths, dec, "cuda", batch_size=4)
+    assert all("error" not in r for r in got), got
+    for p, r in zip(paths, got):
+        alone = transcribe_files(m, [p], dec, "cuda", batch_size=1)[0]
+        assert r == alone

@@ -26,10 +26,17 @@ PEAK_BF16 = 2500e12
 PEAK_F32 = 157.3e12
 
 
-def gemm_rows(path):
+FAMILIES = ("gemm_x3_kernel", "ssm_tail_kernel")
+
+
+def family_rows(path):
+    """{kernel family: [rows sorted by dispatch]} of the counted kernel families."""
+    fam = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if "gemm_x3_kernel" in r["Kernel_Name"]:
-            yield r
+        for f in FAMILIES:
+            if f in r["Kernel_Name"]:
+                fam[f].append(r)
+    return fam
 
 
 def main(tag, Ms):
@@ -38,34 +45,42 @@ def main(tag, Ms):
     md = [f"# MFMA utilisation of the split-bf16 GEMMs ({tag})", "",
           "rocprofv3 counters over `tools/gemm_pmc.py` (isolated launches, random operands), durations from the "
           "un-profiled kernel-trace pass of the same script; `tools/pmc_mfma.sh` + `tools/summarize_mfma.py`.", "",
-          "| M | shape | N | K | dur µs | MFMA flops counted / expected | MFMA TF/s | of 2.5 PF | busy cyc/SIMD | "
-          "busy frac @2.4 GHz | fp32-eq TF/s | of 157.3 TF |", "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+          "| M | shape | kernel | N | K | dur µs | MFMA flops counted / expected | MFMA TF/s | of 2.5 PF | busy cyc/SIMD | "
+          "busy frac @2.4 GHz | fp32-eq TF/s | of 157.3 TF |", "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for M in Ms:
         src = os.path.join(REPO, "gpurun_out", f"mfma_{tag}_{M}")
         order = json.load(open(os.path.join(src, "order.json")))
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                for r in sorted(gemm_rows(os.path.join(src, "trace", "run_kernel_trace.csv")),
-                                key=lambda r: int(r["Dispatch_Id"]))]
-        cnt = collections.defaultdict(dict)
-        for r in gemm_rows(os.path.join(src, "pmc", "run_counter_collection.csv")):
-            d = cnt[int(r["Dispatch_Id"])]
-            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        disp = [cnt[k] for k in sorted(cnt)]
-        per = order[0]["reps"] + 1
-        assert len(durs) == len(disp) == per * len(order), (len(durs), len(disp), per * len(order))
-        for i, sh in enumerate(order):
+        trace = family_rows(os.path.join(src, "trace", "run_kernel_trace.csv"))
+        pmc = family_rows(os.path.join(src, "pmc", "run_counter_collection.csv"))
+        durs = {f: [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"]))] for f, rows in trace.items()}
+        disp = {}
+        for f, rows in pmc.items():
+            cnt = collections.defaultdict(dict)
+            for r in rows:
+                d = cnt[int(r["Dispatch_Id"])]
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            disp[f] = [cnt[k] for k in sorted(cnt)]
+        seen = collections.Counter()
+        for sh in order:
+            f = sh.get("kernel", "gemm_x3_kernel")
+            per = sh["reps"] + 1
+            i = seen[f]
+            seen[f] += 1
             sl = slice(i * per + 1, (i + 1) * per)  # drop the warm-up launch
-            dur = sum(durs[sl]) / (per - 1) * 1e-9
-            c = disp[sl]
+            dur = sum(durs[f][sl]) / (per - 1) * 1e-9
+            c = disp[f][sl]
+            assert len(c) == per - 1, (sh["name"], len(c))
             mops = sum(x["SQ_INSTS_VALU_MFMA_MOPS_BF16"] for x in c) / len(c) * 512
             busy = sum(x["SQ_VALU_MFMA_BUSY_CYCLES"] for x in c) / len(c) / SIMDS
             expect = sh["flops"] * sh["bf16_products"]
-            ent = dict(name=sh["name"], dur_us=round(dur * 1e6, 2), mops_flops=mops, expected_flops=expect,
+            ent = dict(name=sh["name"], kernel=f, dur_us=round(dur * 1e6, 2), mops_flops=mops, expected_flops=expect,
                        mfma_tflops=round(mops / dur / 1e12, 1), mfma_frac=round(mops / dur / PEAK_BF16, 4),
                        busy_per_simd=round(busy), mfma_busy_frac=round(busy / (dur * CLOCK), 4),
                        f32eq_tflops=round(sh["flops"] / dur / 1e12, 2), f32eq_frac=round(sh["flops"] / dur / PEAK_F32, 4))
-            table["%d,%d,%d" % (sh["M"], sh["N"], sh["K"])] = ent
-            md.append(f"| {M} | {sh['name']} | {sh['N']} | {sh['K']} | {ent['dur_us']} | {mops / expect:.3f} | "
+            key = "%d,%d,%d" % (sh["M"], sh["N"], sh["K"]) if f == "gemm_x3_kernel" else "tail,%d" % sh["M"]
+            table[key] = ent
+            md.append(f"| {sh['M']} | {sh['name']} | {f} | {sh['N']} | {sh['K']} | {ent['dur_us']} | {mops / expect:.3f} | "
                       f"{ent['mfma_tflops']} | {ent['mfma_frac']:.3f} | {ent['busy_per_simd']} | "
                       f"{ent['mfma_busy_frac']:.3f} | {ent['f32eq_tflops']} | {ent['f32eq_frac']:.3f} |")
     json.dump(table, open(out_json, "w"), indent=1, sort_keys=True)

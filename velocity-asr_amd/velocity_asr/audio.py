@@ -271,6 +271,13 @@ _STFT_MODE = os.environ.get("VASR_STFT", "fft")
 _STFT_FFT = _STFT_MODE != "gemm"
 
 
+def ragged_supported(n_mels: int = N_MELS, n_fft: int = N_FFT, hop_length: int = HOP_LENGTH) -> bool:
+    """Whether mel_on_device(..., lengths=) can run a zero-padded batch of clips of different
+    lengths: the per-length (_var) kernels exist for the FFT front end of the default geometry
+    with at most 85 mel bins (VASR_STFT=gemm or other geometries raise NotImplementedError)."""
+    return n_fft == 400 and hop_length == 160 and _STFT_FFT and n_mels <= 85
+
+
 def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
                   hop_length: int = HOP_LENGTH, n_mels: int = N_MELS, normalize: bool = True,
                   lengths=None) -> torch.Tensor:
@@ -293,7 +300,7 @@ def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = 
         if len(lengths) != B or not all(pad < v <= S for v in lengths):
             raise RuntimeError(f"compute_mel_spectrogram: lengths must be {B} sample counts in ({pad}, {S}], "
                                f"got {lengths}")
-        if not (n_fft == 400 and hop_length == 160 and _STFT_FFT and n_mels <= 85):
+        if not ragged_supported(n_mels, n_fft, hop_length):
             raise NotImplementedError("per-utterance lengths need the FFT front end (n_fft 400, hop 160, n_mels <= 85)")
         samples = torch.tensor(lengths, dtype=torch.int32).to(x.device)
         frames = torch.tensor([(v + 2 * pad - n_fft) // hop_length + 1 for v in lengths], dtype=torch.int32).to(x.device)

@@ -7,7 +7,8 @@ device pipeline together (mel, forward, argmax, collapse all on the HIP device).
 clips of different lengths is zero-padded to its longest clip and carries each clip's own
 length (pipeline.audio_to_token_ids(..., lengths=)): the mel statistics, pooling sizes,
 attention keys and the collapse follow each clip's length and the SSM stacks are causal, so
-the output for a file is the one the reference's per-file loop produces.
+the output for a file is the one the reference's per-file loop produces.  Where the front end
+has no per-length kernels (VASR_STFT=gemm, n_mels > 85) batches hold clips of one length.
 """
 
 from __future__ import annotations
@@ -19,7 +20,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import torch
 
 from . import ops
-from .audio import HOP_LENGTH, N_FFT, SAMPLE_RATE, load_audio, mel_on_device
+from .audio import HOP_LENGTH, N_FFT, SAMPLE_RATE, load_audio, mel_on_device, ragged_supported
 from .decode import CTCDecoder
 
 logger = logging.getLogger(__name__)
@@ -102,6 +103,22 @@ def _decode_batch(model, audio: torch.Tensor, decoder: CTCDecoder, timestamps: b
     return out
 
 
+def _batches(items: List[Tuple[int, torch.Tensor]], batch_size: int, ragged: bool):
+    """Consecutive batches of the length-sorted items: up to batch_size clips each, zero-padded
+    to the longest when the front end takes per-clip lengths (ragged), else runs of clips of
+    one sample count (the per-length kernels need the FFT front end with n_mels <= 85)."""
+    k = 0
+    while k < len(items):
+        end = min(k + batch_size, len(items))
+        if not ragged:
+            n = items[k][1].numel()
+            end = k + 1
+            while end < len(items) and end - k < batch_size and items[end][1].numel() == n:
+                end += 1
+        yield items[k:end]
+        k = end
+
+
 def transcribe_files(model, paths: Iterable, decoder: CTCDecoder, device, timestamps: bool = False,
                      batch_size: int = 16, beam_width: int = 1) -> List[Dict]:
     """Transcribe audio files; returns one result dict per file in input order.
@@ -126,8 +143,7 @@ def transcribe_files(model, paths: Iterable, decoder: CTCDecoder, device, timest
             results[i] = {"file": p, "error": str(e)}
     dev = torch.device(device)
     items.sort(key=lambda it: it[1].numel())  # neighbours of similar length: little padding
-    for k in range(0, len(items), max(1, batch_size)):
-        chunk = items[k:k + batch_size]
+    for chunk in _batches(items, max(1, batch_size), ragged_supported(model.config.mel_bins)):
         try:
             ns = [a.numel() for _, a in chunk]
             S = max(ns)
