@@ -219,15 +219,88 @@ def cpu_baseline(seconds_target=15.0, chunk=4):
                        f"threads in the build container (SURVEY §6)")
 
 
-def golden_check(toks, lens, args):
-    """Rank 0's tokens vs the reference's greedy lists for the same clips (tests/golden/
-    fwd_fullbatch.npz: make_audio(32, 160000, seed=1234)), when the workload is that batch."""
-    path = os.path.join(REPO, "tests", "golden", "fwd_fullbatch.npz")
-    if args.bf16 or args.int8 or args.batch != 32 or args.seconds != 10.0 or not os.path.exists(path):
+EDIT_BOUND = 0.05  # bf16 token edit rate <= 5 % (the reference's own bf16 drift: 2.3 %)
+
+
+def _edits(a, b):
+    """Levenshtein distance between two token lists (row DP, each row vectorised: the insertion
+    chain cur[j] = min(cur[j - 1] + 1, ...) is a running minimum of cur[k] - k)."""
+    a, b = np.asarray(a, np.int64), np.asarray(b, np.int64)
+    if len(b) == 0:
+        return len(a)
+    ar = np.arange(len(b) + 1)
+    prev = ar.copy()
+    for i, x in enumerate(a, 1):
+        base = np.empty_like(prev)
+        base[0] = i
+        base[1:] = np.minimum(prev[1:] + 1, prev[:-1] + (b != x))
+        prev = np.minimum.accumulate(base - ar) + ar
+    return int(prev[-1])
+
+
+def _golden_lists(kind, rank, seconds, batch):
+    """The reference's greedy token lists for this rank's clips (make_audio(batch, S, 1234 + rank))
+    from tests/golden/ (generated from the reference by tests/golden/gen_goldens.py), as
+    (lists, clips covered), or None.  kind: fp32 | bf16 | int8."""
+    gd = os.path.join(REPO, "tests", "golden")
+    try:
+        full = json.loads(str(np.load(os.path.join(gd, "fwd_fullbatch.npz"), allow_pickle=False)["greedy"]))
+        sets = json.loads(str(np.load(os.path.join(gd, "fwd_benchsets.npz"), allow_pickle=False)["greedy"]))
+    except OSError:
         return None
+    if seconds == 30.0 and kind == "fp32" and rank == 0:
+        ref = full["c4"]  # the first 8 clips of make_audio(32, 480000, seed=1234)
+    elif seconds != 10.0:
+        return None
+    elif kind == "fp32":
+        ref = full["c2"] if rank == 0 else sets.get(f"fp32_r{rank}")
+    else:
+        ref = sets.get(f"{kind}_r{rank}")
+    if ref is None:
+        return None
+    n = min(len(ref), batch)
+    return ref[:n], n
+
+
+def golden_check(toks, lens, args, rank):
+    """This rank's token lists vs the reference's for the same clips: fp32 must be identical
+    (CTC-greedy output identical to the reference, north_star); the bf16 model (C3) and the
+    INT8 fake-quant model (C5) are checked by token edit rate against the reference run with the
+    same numerics (and, for the report, against the fp32 reference).  Returns the counts
+    [ranks with a golden, clips, identical clips, edits, reference tokens, edits vs fp32, pass]."""
     from velocity_asr.pipeline import token_lists
-    g = np.load(path, allow_pickle=False)
-    return token_lists(toks, lens) == json.loads(str(g["greedy"]))["c2"]
+    kind = "bf16" if args.bf16 else "int8" if args.int8 else "fp32"
+    g = _golden_lists(kind, rank, args.seconds, args.batch)
+    if g is None:
+        return [0] * 7
+    ref, n = g
+    got = token_lists(toks[:n], lens[:n])
+    same = sum(a == b for a, b in zip(got, ref))
+    edits = sum(_edits(a, b) for a, b in zip(got, ref))
+    tokens = sum(len(b) for b in ref)
+    e32 = 0
+    if kind != "fp32":
+        r32 = _golden_lists("fp32", rank, args.seconds, args.batch)
+        e32 = sum(_edits(a, b) for a, b in zip(got, r32[0])) if r32 else -1
+    ok = same == n if kind == "fp32" else edits <= EDIT_BOUND * tokens
+    return [1, n, same, edits, tokens, e32, int(ok)]
+
+
+def golden_summary(c, args):
+    """The JSON object of golden_check's counts summed over ranks."""
+    ranks, n, same, edits, tokens, e32, ok = c
+    if not ranks:
+        return None
+    kind = "bf16" if args.bf16 else "int8" if args.int8 else "fp32"
+    out = dict(numerics=kind, ranks_checked=int(ranks), clips=int(n), clips_identical=int(same),
+               token_edit_rate=round(edits / max(tokens, 1), 5), all_ranks_pass=bool(ok == ranks))
+    if kind == "fp32":
+        out["criterion"] = "every clip's greedy token list identical to the reference fp32 CPU path"
+    else:
+        out["criterion"] = (f"token edit rate <= {EDIT_BOUND} vs the reference CPU path run with the same numerics "
+                            f"({'model.to(bfloat16)' if kind == 'bf16' else 'calibrated QAT fake-quant'})")
+        out["token_edit_rate_vs_fp32_reference"] = round(e32 / max(tokens, 1), 5) if e32 >= 0 else None
+    return out
 
 
 def pmc_lookup(name, key=None):
@@ -314,7 +387,10 @@ def run(args):
         from velocity_asr.pipeline import token_lists
         gt, gl = tr.collect()
         graph_match = token_lists(gt, gl) == token_lists(toks, lens)
-    golden_ok = golden_check(toks, lens, args) if rank == 0 else None
+    gc = torch.tensor(golden_check(toks, lens, args, rank), device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(gc)
+    golden = golden_summary([int(v) for v in gc.tolist()], args)
     valid = torch.arange(toks.shape[1], device=dev)[None, :] < lens[:, None]
     csum = torch.tensor([float(lens.sum().item()), float(toks.long().masked_fill(~valid, 0).sum().item())],
                         device=dev, dtype=torch.float64)
@@ -362,7 +438,7 @@ def run(args):
     ms_per_step = elapsed / args.steps * 1e3
     sc, gm = rf.get("scan"), rf["gemm"]
     # GEMM family: split-bf16 ("x3") products = six bf16 MFMA products per fp32 multiply-add
-    x3 = not args.bf16 and os.environ.get("VASR_GEMM", "x3") == "x3"
+    x3 = not args.bf16
     prod = 6 if x3 else 1
     g_ach = prod * gm["top_flops"] / gm["top_t"] / 1e12
     g_f32 = gm["top_flops"] / gm["top_t"] / 1e12
@@ -373,7 +449,7 @@ def run(args):
                        gemm_frac=round(g_ach / BF16_MFMA_PEAK_TFS, 4),
                        gemm_f32eq_tflops=round(g_f32, 2), gemm_f32eq_frac=round(g_f32 / F32_MFMA_PEAK_TFS, 4),
                        gemm_all_f32eq_tflops=round(gm["tflops"], 2))
-    mf = pmc_lookup("pmc_mfma.json")
+    mf = pmc_lookup("pmc_mfma.json") if x3 else None  # counters of the split-bf16 kernels only
     if isinstance(mf, dict):
         ent = mf.get("%d,%d,%d" % gm["top_key"][:3])
         if isinstance(ent, dict):
@@ -437,7 +513,8 @@ def run(args):
         },
         "token_checksum": [int(csum[0].item()), int(csum[1].item())],
         "graph_tokens_match_eager": graph_match,
-        "rank0_tokens_match_reference": golden_ok,
+        "rank0_tokens_match_reference": None if golden is None else bool(golden["all_ranks_pass"]),
+        "tokens_vs_reference": golden,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

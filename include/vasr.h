@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 11
+#define VASR_ABI_VERSION 12
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -42,16 +42,19 @@ extern "C" {
 int vasr_version(void);
 const char* vasr_last_error(void);
 
-/* Runtime helpers: a HIP stream restricted to the CUs set in `mask` (hipExtStreamCreateWithCUMask;
- * bit i = logical CU i) for running independent utterance groups on disjoint parts of the chip,
- * its destruction, and the device's CU count. */
-int vasr_stream_create_cu_mask(const uint32_t* mask, int words, void** stream_out);
-int vasr_stream_destroy(void* stream);
-int vasr_device_cu_count(void);
+/* Tuning options of the launchers (process-wide; not numerics: every setting computes the same
+ * results).  Defaults are read once from the environment variable named per key; 0 = automatic.
+ * vasr_set_option returns the previous value (value < 0 only queries), VASR_EINVAL otherwise. */
+enum vasr_option {
+    VASR_OPT_SCAN_LANES = 0, /* state indices per lane of vasr_ssm_scan_f32: 0, 2, 4 (VASR_SCAN_NPL)       */
+    VASR_OPT_SCAN_CHUNK = 1, /* time steps per staged chunk of the streaming scan: 0, 16, 32 (VASR_SCAN_T) */
+    VASR_OPT_TAIL_ROWS = 2   /* token rows per fused-SSMBlock-tail workgroup: 0, 16, 32 (VASR_TAIL_ROWS)   */
+};
+int vasr_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ GEMM
  * C[b] = epilogue(A[b] (M x K) * W^T (K x N) + bias), W row-major [N][K] as in
- * nn.Linear.  fp32 in / fp32 accumulate on v_mfma_f32_32x32x2f32.
+ * nn.Linear, fp32 in / fp32 out (vasr_linear_x3_f32), or bf16 weights (vasr_linear_bf16).
  * Replaces every nn.Linear / Conv1d-as-GEMM on the path: in_proj, x_proj+dt_proj
  * (ssm.py:72-79, :105-113), out_proj (:90, :130), FFN (:394-400), temporal conv
  * (model.py:156-162), pool_proj (attention.py:35, :76), q/k/v/out (:107-110),
@@ -94,33 +97,15 @@ typedef struct vasr_gemm_args {
                                global_proj) followed by n_out entries for local_proj.
                                A column whose scale is 0 is not quantized.  Not allowed
                                with PAIR_POWER. */
-    /* ln_w / ln_b: NULL, or LayerNorm each A row over its K columns first:
-       A'[r][k] = (A[r][k] - mean_r) * rstd_r * ln_w[k] + ln_b[k], rstd_r = 1/sqrt(var_r + ln_eps)
-       (nn.LayerNorm(K) feeding the Linear: SSMBlock norm2 -> FFN, ssm.py:394-427; CTC head LN,
-       model.py:218-227).  The same float operations as vasr_layer_norm_f32, so the product
-       equals LN-then-GEMM bit for bit.  vasr_linear_x3_f32 / vasr_linear_bf16 only,
-       K % 32 == 0, K <= 384, epilogues NONE / GELU / RESIDUAL / ARGMAX. */
-    const float* ln_w;
-    const float* ln_b;
-    float ln_eps;
 } vasr_gemm_args;
 
-int vasr_linear_f32(const vasr_gemm_args* args, void* stream);
-
-/* The same GEMM (same args, epilogues and results to within fp32 accumulation order) on
- * the bf16 matrix cores: fp32 operands are split exactly into three bf16 terms
- * (x = hi + mid + lo, all 24 significant bits) and the six products larger than
- * 2^-25 |a||b| are accumulated in fp32 on v_mfma_f32_32x32x16_bf16 — 2.67x the
- * f32-input MFMA rate.  `w_split` holds W pre-split by vasr_split_weights_bf16x3
- * (args->W is not read).  Replaces the same reference ops as vasr_linear_f32.
+/* The fp32 GEMM (fp32 results to within accumulation order) on the bf16 matrix cores: fp32
+ * operands are split exactly into three bf16 terms (x = hi + mid + lo, all 24 significant
+ * bits) and the six products larger than 2^-25 |a||b| are accumulated in fp32 on
+ * v_mfma_f32_32x32x16_bf16 — 2.67x the f32-input MFMA rate.  `w_split` holds W pre-split by
+ * vasr_split_weights_bf16x3 (args->W is not read).
  */
 int vasr_linear_x3_f32(const vasr_gemm_args* args, const uint16_t* w_split, void* stream);
-/* Main-loop selection of vasr_linear_x3_f32 (same MFMA sequence, bit-identical results):
- * 0 (default) = LDS-ring tiles; 1 / 2 (or env VASR_GEMM_PANEL=1 / 2) = LDS-resident 64-column
- * weight panels with A streamed through registers at 4 / 2 waves per SIMD, used where
- * K = 192 or 384 and the epilogue is unpaired (measured slower overall; experimental).
- * Returns the previous setting; other values only query. */
-int vasr_set_x3_engine(int engine);
 
 /* Split W (N x K fp32, row stride ldw) into bf16 terms (hi, mid, lo) in the fragment-native
  * layout out[NT][KS][3][64][8] (NT = ceil(N/32), KS = Kp/16, Kp = K rounded up to 32):
@@ -135,7 +120,7 @@ int64_t vasr_split_weights_elems(int N, int K);
  * fp32 in HBM and is rounded to bf16 (round-to-nearest-even) as it enters the MFMA
  * (v_mfma_f32_32x32x16_bf16), accumulation and epilogues in fp32 — the reference's bf16
  * Linear (ssm.py, attention.py, model.py nn.Linear under bf16 parameters) with fp32
- * accumulation.  Same args and epilogues as vasr_linear_f32. */
+ * accumulation.  Same args and epilogues as vasr_linear_x3_f32. */
 int vasr_linear_bf16(const vasr_gemm_args* args, const uint16_t* w_packed, void* stream);
 int vasr_pack_weights_bf16(const uint16_t* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
 int64_t vasr_pack_weights_bf16_elems(int N, int K);
@@ -208,19 +193,6 @@ int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x, int64_t
                             const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
                             const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
                             int M, int D, int E, void* stream);
-/* The head of SSMBlock._forward_impl + SelectiveSSM's projections (ssm.py:404-414, :105-113)
- * in one launch for d_model D = 192, d_inner Di = 384, Nx = 2N + Di = 512 (N = 64):
- *   u = causal_dwconv4(LayerNorm(x; ln_w, ln_b, ln_eps); conv_w (D, 4), conv_b), per utterance
- *       of L tokens (M = B * L rows);
- *   xz = u @ Win^T -> (M, 2 Di) [x_p | z];  xdt = x_p @ Wxd^T + bxd, softplus on columns >= n_sp
- *       -> (M, Nx) [B | C | dt]
- * Win / Wxd as vasr_split_weights16_bf16x3 planes (bf16 = 0) or vasr_pack_weights16_bf16 planes
- * of bf16 weights (bf16 = 1: the bf16 model's arithmetic).  u never leaves the chip. */
-int vasr_ssm_block_head_f32(const float* x, int64_t ldx, const float* ln_w, const float* ln_b, float ln_eps,
-                            const float* conv_w, const float* conv_b, const uint16_t* win16,
-                            const uint16_t* wxd16, const float* bxd, int n_sp, float* xz, int64_t ldxz,
-                            float* xdt, int64_t ldxdt, int M, int L, int D, int Di, int Nx, int bf16,
-                            void* stream);
 /* The same tail for the bf16 model (C3): weights as one bf16 plane (vasr_pack_weights16_bf16 of
  * the bf16 parameters), activations rounded to bf16 at the MFMA input, fp32 accumulation and
  * fp32 LayerNorm / bias / GELU / residual -- the arithmetic of vasr_linear_bf16. */
@@ -253,12 +225,15 @@ int vasr_resample_f32(const float* x, int channels, int64_t n, int64_t ld_x, int
  * compute_mel_spectrogram (audio.py:65-143) is three launches:
  *  1. vasr_reflect_pad_f32: xp[b][0:S+2*pad] = reflect-padded audio (audio.py:100-101),
  *     rows of stride ld_out (>= S + 2*pad + n_fft); the tail is zero-filled.
- *  2. vasr_linear_f32 with VASR_EPI_PAIR_POWER on rows of stride `hop` of xp against the
+ *  2. vasr_linear_x3_f32 with VASR_EPI_PAIR_POWER on rows of stride `hop` of xp against the
  *     Hann-windowed DFT matrix -> power[b][f][k] = |X_k|^2 (audio.py:104-115).
  *  3. vasr_mel_log_norm_f32: mel = fb @ power (audio.py:126), log(mel + 1e-10) (:129),
  *     per-(b, mel bin) (x - mean)/(std_unbiased + 1e-10) over frames (:132-135), written
- *     to out[b][frame_off + f][m] with batch stride out_stride (frames of a padded
- *     layout are left untouched).  fb is passed in CSR form (rows = mel bins).
+ *     to out[b][frame_off + f][m] with batch stride out_stride.  The other frames of each
+ *     utterance's padded slab of out_stride / n_mels frames are written as 0: the zero-framed
+ *     (B, F + 2, n_mels) layout the stride-2 temporal conv GEMM reads as plain strided rows
+ *     (model.py:156-162, padding 1), with no separate padding pass.  fb is passed in CSR form
+ *     (rows = mel bins).
  */
 int vasr_reflect_pad_f32(const float* audio, int64_t ld_audio, float* xp, int64_t ld_out,
                          int B, int S, int pad, void* stream);
@@ -293,20 +268,10 @@ int vasr_stft_power_400_f32(const float* audio, int64_t ld_audio, int B, int S, 
 int vasr_stft_power_400_var_f32(const float* audio, int64_t ld_audio, int B, int S, const int32_t* samples,
                                 const float* window, float* power, int64_t ldp, int64_t stride_power,
                                 void* stream);
-/* The whole front end for n_fft = 400, hop = 160 with the power spectrum kept on chip: the
- * real FFT above for one 16-frame chunk per workgroup, then in the same workgroup mel + log
- * of the chunk and its per-bin fp64 partials, then the stats / normalisation passes of
- * vasr_mel_log_norm_f32 (same workspace, same outputs bit for bit as stft_power + mel_log_norm).
- * n_mels <= 85; out / out_stride / frame_off / normalize as in vasr_mel_log_norm_f32.
- * Measured slower than the two-step form (39.9 vs 35.4 us for 16 x 10 s): opt-in. */
-int vasr_stft_logmel_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
-                             const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
-                             float* out, int64_t out_stride, int frame_off, int n_mels, int normalize,
-                             float* workspace, void* stream);
-
 /* Write (B, F, C) rows into a zero-padded frame layout: out[b][off + f][c] = x[b][f][c]
  * and zero for the other out_frames - F frames (batch stride out_frames * C).  Feeds mel
- * to the stride-2 temporal conv, whose im2col rows are then plain strided rows. */
+ * to the stride-2 temporal conv, whose im2col rows are then plain strided rows (the public
+ * model(mel) path; the device pipeline has vasr_mel_log_norm_f32 write the padded layout). */
 int vasr_pad_frames_f32(const float* x, float* out, int out_frames, int off,
                         int B, int F, int C, void* stream);
 

@@ -48,3 +48,33 @@ def record_error(got, want, tol):
                tol_use=float((d / (tol["atol"] + tol["rtol"] * np.abs(want))).max()) if d.size else 0.0)
     with open(path, "a") as f:
         f.write(json.dumps(rec) + "\n")
+
+
+def edit_distance(a, b):
+    """Levenshtein distance between two token lists (row DP, each row vectorised)."""
+    a, b = np.asarray(a, np.int64), np.asarray(b, np.int64)
+    if len(b) == 0:
+        return len(a)
+    ar = np.arange(len(b) + 1)
+    prev = ar.copy()
+    for i, x in enumerate(a, 1):
+        base = np.empty_like(prev)
+        base[0] = i
+        base[1:] = np.minimum(prev[1:] + 1, prev[:-1] + (b != x))
+        prev = np.minimum.accumulate(base - ar) + ar
+    return int(prev[-1])
+
+
+def token_edit_rate(got, ref):
+    """Summed edit distance of token lists over the summed reference length (a token-level WER)."""
+    return sum(edit_distance(a, b) for a, b in zip(got, ref)) / max(1, sum(len(b) for b in ref))
+
+
+def record_metric(name, **values):
+    """Append {test, name, values} to $VASR_PARITY_LOG when set (measured rates for DESIGN.md)."""
+    path = os.environ.get("VASR_PARITY_LOG")
+    if not path:
+        return
+    rec = dict(test=os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], name=name, **values)
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")

@@ -6,20 +6,21 @@ weights and bf16 MFMA operands but accumulates in fp32 and keeps activations fp3
 kernels, so it sits between the reference's bf16 and fp32 outputs.
 
 Tolerances (SURVEY §8d for bf16): logits max-abs <= 0.1; per-frame argmax agreement >= 95 %
-and greedy token-sequence similarity >= 0.9 against both the reference bf16 golden and the
-fp32 golden (the reference's own bf16-vs-fp32 drift: max 0.030, argmax agreement 98.0 %).
+and token edit rate of the greedy lists <= 5 % against both the reference bf16 golden and the
+fp32 golden (the reference's own bf16-vs-fp32 drift: max 0.030, argmax agreement 98.0 %, edit
+rate 2.2-2.5 % on the bench batches).  The bench-shape batches (32 x 10 s per rank, C3) are in
+tests/test_bench_workloads.py.
 GEMM kernel: fp32 accumulation of exact bf16 products, vs float64 of the same rounded
 operands: max-abs <= 2e-5 * scale.
 """
 
-import difflib
 import json
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import golden, golden_json
+from conftest import golden, golden_json, record_metric, token_edit_rate
 from oracle import velocity_ref as R
 from velocity_asr import synthetic as S
 
@@ -67,9 +68,10 @@ def test_gemm_bf16(va, M, N, K, epi):
 
 def _check(logits, tokens_ref, greedy_ref, gold_logits=None, sub=1):
     agree = float((logits.argmax(-1) == tokens_ref).mean())
-    sims = [difflib.SequenceMatcher(a=a, b=b).ratio() for a, b in zip(greedy_ref, R.ctc_greedy_decode(logits))]
+    rate = token_edit_rate(R.ctc_greedy_decode(logits), greedy_ref)
+    record_metric("bf16_small", argmax_agreement=agree, token_edit_rate=rate)
     assert agree >= 0.95, f"argmax agreement {agree:.4f}"
-    assert min(sims) >= 0.9, f"greedy similarity {sims}"
+    assert rate <= 0.05, f"token edit rate {rate:.4f}"
     d = None
     if gold_logits is not None:
         d = float(np.abs(logits[:, ::sub] - gold_logits).max())

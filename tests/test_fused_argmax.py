@@ -24,7 +24,7 @@ def va():
     return velocity_asr
 
 
-@pytest.mark.parametrize("engine", ["x3", "f32", "bf16"])
+@pytest.mark.parametrize("engine", ["x3", "bf16"])
 @pytest.mark.parametrize("M,N,K", [(1, 64, 32), (77, 1000, 192), (16032, 1000, 192), (300, 50, 96), (129, 257, 192)])
 def test_gemm_argmax_matches_logits(va, engine, M, N, K):
     from velocity_asr import ops
@@ -39,14 +39,10 @@ def test_gemm_argmax_matches_logits(va, engine, M, N, K):
     a[: M // 2] *= 0.0                # rows whose logits are the bias alone (ties on bias)
     if engine == "bf16":
         w = w.to(torch.bfloat16)
-    prev = ops.set_gemm_mode("x3" if engine == "bf16" else engine)
-    try:
-        A, W, Bv = a.to(DEV), w.to(DEV), b.to(DEV)
-        logits = ops.gemm(A, W, Bv)
-        want = torch.argmax(logits, dim=-1).to(torch.int32).cpu()
-        got = ops.gemm_argmax(A, W, Bv).cpu()
-    finally:
-        ops.set_gemm_mode(prev)
+    A, W, Bv = a.to(DEV), w.to(DEV), b.to(DEV)
+    logits = ops.gemm(A, W, Bv)
+    want = torch.argmax(logits, dim=-1).to(torch.int32).cpu()
+    got = ops.gemm_argmax(A, W, Bv).cpu()
     assert torch.equal(got, want)
 
 

@@ -18,7 +18,7 @@ from velocity_asr import synthetic as S
 def test_c_abi_library_exports_every_header_symbol():
     from velocity_asr import _lib
     names = _lib.header_functions()
-    assert "vasr_ssm_scan_f32" in names and "vasr_linear_f32" in names
+    assert "vasr_ssm_scan_f32" in names and "vasr_linear_x3_f32" in names
     lib = ctypes.CDLL(_lib.LIB_PATH)
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
@@ -40,21 +40,34 @@ def test_abi_rejects_bad_arguments_without_gpu():
     rc = L.vasr_ctc_collapse(None, 1, 1, 0, 1, None, None, None, None, None)
     assert rc == -1
     args = _lib.GemmArgs()
-    assert L.vasr_linear_f32(ctypes.byref(args), None) == -1
     assert L.vasr_linear_x3_f32(ctypes.byref(args), None, None) == -1
+    assert L.vasr_linear_bf16(ctypes.byref(args), None, None) == -1
     assert L.vasr_split_weights_bf16x3(None, 4, 4, 4, None, None) == -1
     assert L.vasr_split_weights_elems(70, 100) == 3 * 96 * 128
     # front end: null pointers and too-short audio are rejected before any launch
     assert L.vasr_stft_power_400_f32(None, 0, 1, 1000, None, None, 201, 201, None) == -1
-    assert L.vasr_stft_logmel_400_f32(None, 0, 1, 1000, None, None, None, None, None, 0, 0, 80, 1, None, None) == -1
-    # the row-LayerNorm prologue is refused by the f32 engine and needs K % 32 == 0
+    # GEMM shape rules: K a multiple of 4
     args = _lib.GemmArgs()
-    args.A = args.C = args.W = args.ln_w = args.ln_b = 16
-    args.batch, args.M, args.N, args.K, args.lda, args.ldw, args.ldc = 1, 4, 4, 36, 36, 36, 4
-    assert L.vasr_linear_f32(ctypes.byref(args), None) == -1
-    assert b"LayerNorm" in L.vasr_last_error()
-    # engine switch: query only (values outside 0..2 change nothing)
-    assert L.vasr_set_x3_engine(-1) == L.vasr_set_x3_engine(-1)
+    args.A = args.C = args.W = 16
+    args.batch, args.M, args.N, args.K, args.lda, args.ldw, args.ldc = 1, 4, 4, 34, 36, 36, 4
+    assert L.vasr_linear_x3_f32(ctypes.byref(args), 16, None) == -1
+    assert b"multiples of 4" in L.vasr_last_error()
+
+
+def test_tuning_options():
+    """vasr_set_option: launcher decomposition knobs (never numerics), query with value < 0,
+    unknown keys / values refused."""
+    from velocity_asr import _lib, ops
+    L = _lib.load()
+    for key, allowed in ((_lib.OPT_SCAN_LANES, (2, 4)), (_lib.OPT_SCAN_CHUNK, (16, 32)), (_lib.OPT_TAIL_ROWS, (16, 32))):
+        base = L.vasr_set_option(key, -1)
+        assert base in (0,) + allowed
+        for v in allowed:
+            with ops.option(key, v):
+                assert L.vasr_set_option(key, -1) == v
+            assert L.vasr_set_option(key, -1) == base
+        assert L.vasr_set_option(key, 3) == -1 and b"not allowed" in L.vasr_last_error()
+    assert L.vasr_set_option(7, 0) == -1 and b"unknown option" in L.vasr_last_error()
 
 
 def test_public_api_matches_reference_all():

@@ -14,19 +14,19 @@ Tolerances:
     step (~0.02-0.03 here) and the SSM recurrence carries that forward in time, so two
     correct implementations (the numpy oracle vs torch CPU, measured: mean |dlogit| 2.9e-3,
     max 0.038, per-frame argmax 97.7 % equal) differ at the quantisation-step level.
-    Bounds: per-frame argmax agreement >= 95 %, greedy token sequence similarity >= 0.9,
-    mean |dlogit| <= 0.01, max |dlogit| <= 0.15.
+    Bounds: per-frame argmax agreement >= 95 %, token edit rate of the greedy lists <= 5 %,
+    mean |dlogit| <= 0.01, max |dlogit| <= 0.15.  The bench-shape batch (32 x 10 s, C5) is in
+    tests/test_bench_workloads.py.
   * calibrate_model (the reference's own, with its scale-1 defect): logits identical (0).
 """
 
-import difflib
 import json
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import golden, record_metric, token_edit_rate
 from oracle import velocity_ref as R
 from velocity_asr import synthetic as S
 
@@ -52,9 +52,10 @@ def _qat_state(z):
 def _statistical_check(logits, tokens_ref, greedy_ref, gold_logits, greedy_fn):
     d = np.abs(logits - gold_logits)
     agree = float((logits.argmax(-1) == tokens_ref).mean())
-    sims = [difflib.SequenceMatcher(a=a, b=b).ratio() for a, b in zip(greedy_ref, greedy_fn(logits))]
+    rate = token_edit_rate(greedy_fn(logits), greedy_ref)
+    record_metric("int8_small", argmax_agreement=agree, token_edit_rate=rate, max_abs=float(d.max()))
     assert agree >= 0.95, f"per-frame argmax agreement {agree:.3f}"
-    assert min(sims) >= 0.9, f"greedy sequence similarity {sims}"
+    assert rate <= 0.05, f"token edit rate {rate:.4f}"
     assert d.mean() <= 0.01 and d.max() <= 0.15, f"mean |d| {d.mean():.4f}, max {d.max():.4f}"
     return agree, d
 
@@ -171,27 +172,22 @@ def test_gpu_minmax_nan_and_extremes(va):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("engine", ["x3", "f32"])
 @pytest.mark.parametrize("M,N,K", [(77, 48, 192), (300, 192, 192), (129, 1000, 192)])
-def test_gpu_gemm_quant_epilogue_bit_exact(va, engine, M, N, K):
+def test_gpu_gemm_quant_epilogue_bit_exact(va, M, N, K):
     """acc + bias -> fake-quant in the epilogue == the oracle's fake_quantize of the raw GEMM output."""
     from velocity_asr import ops
-    prev = ops.set_gemm_mode(engine)
-    try:
-        rng = np.random.default_rng(M + N)
-        a = rng.standard_normal((M, K)).astype(np.float32)
-        w = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
-        b = (rng.standard_normal(N) * 0.1).astype(np.float32)
-        raw = ops.gemm(_t(a), _t(w), _t(b)).cpu().numpy()
-        scale, zp = R.observe_scale_zp(raw, False, False, 0, 255)
-        qp = np.tile(np.array([[scale, zp, 0, 255]], np.float32), (N, 1))
-        qp[3] = 0.0  # column 3 passes through (scale 0)
-        got = ops.gemm(_t(a), _t(w), _t(b), qparams=_t(qp)).cpu().numpy()
-        want = R.fake_quantize(raw, scale, zp, 0, 255)
-        want[:, 3] = raw[:, 3]
-        assert np.array_equal(got.view(np.int32), want.view(np.int32))
-    finally:
-        ops.set_gemm_mode(prev)
+    rng = np.random.default_rng(M + N)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    w = (rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
+    b = (rng.standard_normal(N) * 0.1).astype(np.float32)
+    raw = ops.gemm(_t(a), _t(w), _t(b)).cpu().numpy()
+    scale, zp = R.observe_scale_zp(raw, False, False, 0, 255)
+    qp = np.tile(np.array([[scale, zp, 0, 255]], np.float32), (N, 1))
+    qp[3] = 0.0  # column 3 passes through (scale 0)
+    got = ops.gemm(_t(a), _t(w), _t(b), qparams=_t(qp)).cpu().numpy()
+    want = R.fake_quantize(raw, scale, zp, 0, 255)
+    want[:, 3] = raw[:, 3]
+    assert np.array_equal(got.view(np.int32), want.view(np.int32))
 
 
 @pytest.mark.gpu

@@ -163,3 +163,25 @@ def test_length_checks(va, model):
     mel = mel_on_device(audio, lengths=[1000, 500])
     with pytest.raises(ValueError, match="frames"):
         model(mel, frames=[7, 0])
+
+
+@pytest.mark.parametrize("lengths", [None, [16000, 9000, 12345]])
+def test_zero_framed_mel_feeds_the_conv_in_place(va, model, lengths):
+    """the pipeline's mel is written into a zero-framed (B, F + 2, 80) buffer
+    by the normalisation pass (no padding kernel); the view equals compute_mel_spectrogram bit
+    for bit, the outer frames are 0, and the model's outputs on it equal those on the plain mel."""
+    from velocity_asr import ops
+    from velocity_asr.audio import mel_on_device
+    audio = torch.from_numpy(S.make_audio(3, 16000, seed=77)).to(DEV)
+    if lengths is not None:
+        for b, n in enumerate(lengths):
+            audio[b, n:] = 0
+    plain = mel_on_device(audio, lengths=lengths)
+    framed = mel_on_device(audio, lengths=lengths, frame_pad=1)
+    assert torch.equal(framed, plain)
+    buf = ops.zero_framed(framed, 1)
+    assert buf is not None and tuple(buf.shape) == (3, plain.shape[1] + 2, 80)
+    assert not buf[:, 0].any() and not buf[:, -1].any()
+    frames = None if lengths is None else [n // 160 + 1 for n in lengths]
+    assert torch.equal(model(framed, frames=frames), model(plain.clone(), frames=frames))
+    assert ops.zero_framed(plain, 1) is None and ops.zero_framed(framed.clone(), 1) is None

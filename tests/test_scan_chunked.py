@@ -42,17 +42,28 @@ def _silu(z):
     return z / (1.0 + np.exp(-z.astype(np.float64)))
 
 
+def _form(form, fn, *a):
+    from velocity_asr import ops
+    prev = ops.scan_form(form)
+    try:
+        return fn(*a)
+    finally:
+        ops.scan_form(prev)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 2])
-@pytest.mark.parametrize("npl", ["2", "4"])
+@pytest.mark.parametrize("npl", [2, 4])
+@pytest.mark.parametrize("tc", [16, 32])
 @pytest.mark.parametrize("B,L", [(1, 1), (1, 17), (2, 17), (1, 501), (2, 501), (1, 1501), (2, 2049), (1, 4100), (1, 8192)])
-def test_chunked_bitwise_equals_streaming(monkeypatch, mode, npl, B, L):
-    monkeypatch.setenv("VASR_SCAN_NPL", npl)
+def test_chunked_bitwise_equals_streaming(mode, npl, tc, B, L):
+    """The chunk-parallel form equals the streaming kernel bit for bit, with either streaming
+    chunk length (16 / 32 steps: the same float operations) and either lane layout."""
+    from velocity_asr import _lib, ops
     args = _inputs(31 * L + B, B, L, 64, 64)
-    monkeypatch.setenv("VASR_SCAN_CHUNKED", "0")
-    stream = _run(*args, mode)
-    monkeypatch.setenv("VASR_SCAN_CHUNKED", "1")
-    chunk = _run(*args, mode)
+    with ops.option(_lib.OPT_SCAN_LANES, npl), ops.option(_lib.OPT_SCAN_CHUNK, tc):
+        stream = _form("streaming", _run, *args, mode)
+        chunk = _form("chunked", _run, *args, mode)
     np.testing.assert_array_equal(chunk, stream)
     if L <= 2049:
         x, dt, Bm, Cm, A_log, D, z = args
@@ -61,14 +72,14 @@ def test_chunked_bitwise_equals_streaming(monkeypatch, mode, npl, B, L):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tc", [16, 32])
 @pytest.mark.parametrize("N,Di", [(16, 64), (32, 384), (64, 384)])
-def test_chunked_state_dims_and_model_width(monkeypatch, N, Di):
-    monkeypatch.setenv("VASR_SCAN_NPL", "4")
+def test_chunked_state_dims_and_model_width(tc, N, Di):
+    from velocity_asr import _lib, ops
     args = _inputs(7 * N, 1, 300, Di, N)
-    monkeypatch.setenv("VASR_SCAN_CHUNKED", "0")
-    stream = _run(*args, 2)
-    monkeypatch.setenv("VASR_SCAN_CHUNKED", "1")
-    np.testing.assert_array_equal(_run(*args, 2), stream)
+    with ops.option(_lib.OPT_SCAN_LANES, 4), ops.option(_lib.OPT_SCAN_CHUNK, tc):
+        stream = _form("streaming", _run, *args, 2)
+        np.testing.assert_array_equal(_form("chunked", _run, *args, 2), stream)
 
 
 @pytest.mark.gpu
@@ -86,7 +97,6 @@ def test_chunked_is_the_default_for_one_utterance():
 def test_one_utterance_30s_tokens_match_reference():
     """B = 1 x 30 s through the chunked scan: argmax tokens equal the reference golden
     (fwd_b1_30s.npz) and the streaming form's logits bit for bit."""
-    import os
     import velocity_asr as va
     from conftest import golden
     from velocity_asr import synthetic as S
@@ -95,15 +105,10 @@ def test_one_utterance_30s_tokens_match_reference():
     m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
     m = m.to(DEV).eval()
     mel = va.compute_mel_spectrogram(torch.from_numpy(S.make_audio(1, 480000, seed=4321)).to(DEV))
-    os.environ["VASR_SCAN_CHUNKED"] = "1"
-    os.environ["VASR_SCAN_NPL"] = "4"  # the same lane layout for both forms: bitwise comparable
-    try:
-        lc = m(mel)
-        os.environ["VASR_SCAN_CHUNKED"] = "0"
-        ls = m(mel)
-    finally:
-        os.environ.pop("VASR_SCAN_CHUNKED", None)
-        os.environ.pop("VASR_SCAN_NPL", None)
+    from velocity_asr import _lib, ops
+    with ops.option(_lib.OPT_SCAN_LANES, 4):  # the same lane layout for both forms: bitwise comparable
+        lc = _form("chunked", m, mel)
+        ls = _form("streaming", m, mel)
     assert torch.equal(lc, ls)
     np.testing.assert_array_equal(lc.argmax(-1).cpu().numpy(), golden("fwd_b1_30s.npz")["tokens"])
 

@@ -1,5 +1,8 @@
-// Error state and version entry points of libvasr_hip.so.
+// Error state, version and tuning-option entry points of libvasr_hip.so.
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "vasr_internal.h"
@@ -23,33 +26,42 @@ VASR_API int vasr_version(void) { return VASR_ABI_VERSION; }
 
 VASR_API const char* vasr_last_error(void) { return vasr::g_last_error; }
 
-// A stream whose kernels run only on the CUs set in `mask` (bit i = logical CU i, `words`
-// uint32 words), on the current device: lets two independent utterance groups each own part
-// of the chip instead of competing for every CU.
-VASR_API int vasr_stream_create_cu_mask(const uint32_t* mask, int words, void** stream_out) {
-    VASR_CHECK_ARG(mask && words > 0 && stream_out, "vasr_stream_create_cu_mask: bad arguments");
-    hipStream_t s = nullptr;
-    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
-    if (e != hipSuccess) {
-        vasr::set_error("vasr_stream_create_cu_mask: %s", hipGetErrorString(e));
-        return (int)e;
-    }
-    *stream_out = s;
-    return VASR_OK;
+// Tuning options (vasr_set_option): process-wide, defaults from the environment read once.
+namespace {
+constexpr int kNumOptions = 3;
+const char* const kOptionEnv[kNumOptions] = {"VASR_SCAN_NPL", "VASR_SCAN_T", "VASR_TAIL_ROWS"};
+const int kOptionValues[kNumOptions][3] = {{0, 2, 4}, {0, 16, 32}, {0, 16, 32}};
+std::atomic<int> g_options[kNumOptions];
+std::once_flag g_options_once;
+
+bool option_value_ok(int key, int v) {
+    for (int a : kOptionValues[key])
+        if (v == a) return true;
+    return false;
 }
 
-VASR_API int vasr_stream_destroy(void* stream) {
-    const hipError_t e = hipStreamDestroy(reinterpret_cast<hipStream_t>(stream));
-    if (e != hipSuccess) {
-        vasr::set_error("vasr_stream_destroy: %s", hipGetErrorString(e));
-        return (int)e;
-    }
-    return VASR_OK;
+void options_init() {
+    std::call_once(g_options_once, [] {
+        for (int k = 0; k < kNumOptions; ++k) {
+            const char* e = std::getenv(kOptionEnv[k]);
+            const int v = e ? std::atoi(e) : 0;
+            g_options[k].store(option_value_ok(k, v) ? v : 0, std::memory_order_relaxed);
+        }
+    });
 }
+}  // namespace
 
-VASR_API int vasr_device_cu_count(void) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-    return n;
+namespace vasr {
+int option(int key) {
+    options_init();
+    return g_options[key].load(std::memory_order_relaxed);
+}
+}  // namespace vasr
+
+VASR_API int vasr_set_option(int key, int value) {
+    VASR_CHECK_ARG(key >= 0 && key < kNumOptions, "vasr_set_option: unknown option %d", key);
+    options_init();
+    if (value < 0) return g_options[key].load(std::memory_order_relaxed);
+    VASR_CHECK_ARG(option_value_ok(key, value), "vasr_set_option: value %d not allowed for option %d", value, key);
+    return g_options[key].exchange(value, std::memory_order_relaxed);
 }

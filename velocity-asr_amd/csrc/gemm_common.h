@@ -1,7 +1,6 @@
-// Pieces shared by the two GEMM main loops (gemm_f32.hip: f32-input MFMA; gemm_x3.hip:
-// split-bf16 MFMA): parameters, the XCD-aware tile decode, the fused epilogues and the
-// tile-configuration cost model.  Both main loops leave the same accumulator layout —
-// the 32x32 C/D map is dtype-independent on gfx950 — so one epilogue serves both.
+// Pieces of the GEMM (gemm_x3.hip: split-bf16 and bf16 MFMA main loops): parameters, the
+// XCD-aware tile decode, the fused epilogues and argument checks.  The 32x32 accumulator
+// map of v_mfma_f32_32x32x16_bf16 is the one the epilogues index.
 #pragma once
 
 #include "vasr_internal.h"
@@ -32,9 +31,6 @@ struct GemmParams {
     int n_out;
     const float4* qp;  // per-column activation fake-quant {scale, zp, qmin, qmax} or null
     int batch;
-    const float* ln_w;  // LayerNorm of each A row over K (weight, bias) before the product, or null
-    const float* ln_b;
-    float ln_eps;
 };
 
 struct Tile {
@@ -283,28 +279,6 @@ struct TileCfg {
     int bn() const { return wn * 32 * tn; }
 };
 constexpr int kCUs = 256;
-constexpr int kLnMaxK = 384;  // row-LayerNorm prologue: K (= the normalised width) limit
-
-// Pick the tile that minimises (rounds of resident blocks) x (blocks sharing a CU) x tile area:
-// at M = 16032 the grids are only one or two rounds deep, so wave quantisation and CU
-// balance, not per-tile efficiency, decide the time (measured in tools/gemm_variants_run.py).
-inline int pick_cfg(const TileCfg* cfgs, int n, int M, int N, int batch, bool pair) {
-    int best = -1;
-    double best_cost = 0;
-    for (int i = 0; i < n; ++i) {
-        const TileCfg& c = cfgs[i];
-        if (pair && c.tn % 2 != 0) continue;
-        const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
-        const long per_cu = (tiles + kCUs - 1) / kCUs;
-        const long rounds = (per_cu + c.occ - 1) / c.occ;
-        const double cost = (double)rounds * (double)(per_cu < c.occ ? per_cu : c.occ) * c.bm() * c.bn();
-        if (best < 0 || cost < best_cost * 0.999) {
-            best = i;
-            best_cost = cost;
-        }
-    }
-    return best;
-}
 
 // Argument checks common to both GEMM entry points; fills p (W / Wx left to the caller).
 inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
@@ -339,19 +313,8 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
     p.aux2 = a->aux2; p.n_out = a->n_out;
     p.qp = reinterpret_cast<const float4*>(a->qparams);
     p.batch = a->batch;
-    p.ln_w = a->ln_w;
-    p.ln_b = a->ln_b;
-    p.ln_eps = a->ln_eps;
-    if (a->ln_w)
-        VASR_CHECK_ARG(a->ln_b != nullptr && a->K % 32 == 0 && a->K <= kLnMaxK,
-                       "%s: row LayerNorm needs ln_b, K %% 32 == 0 and K <= %d (K=%d)", fn, kLnMaxK, a->K);
     return VASR_OK;
 }
-
-// gemm_panel.hip: launches the LDS-resident-panel split GEMM when it is enabled and the shape
-// suits it (K = 192 / 384, unpaired epilogues) and returns true with the launch status in *rc;
-// false when not eligible (the tile kernel runs instead).
-bool try_panel_x3(const GemmParams& p, int epi, hipStream_t st, int* rc);
 
 }  // namespace gemm
 }  // namespace vasr

@@ -84,10 +84,7 @@ constexpr int x3_occ() {
     return 163840 / lds >= cap ? cap : (163840 / lds >= 1 ? 163840 / lds : 1);
 }
 
-// LNA: LayerNorm each A row over K before the product (GemmParams::ln_w / ln_b / ln_eps): the
-// block computes its rows' mean / rstd once (the float operations of vasr_layer_norm_f32) and
-// normalises every A fragment after its LDS read, before the split; LN weights sit in LDS.
-template <int WM, int WN, int TM, int TN, int RING, int EPI, int P, bool LNA = false>
+template <int WM, int WN, int TM, int TN, int RING, int EPI, int P>
 __global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm_x3_kernel(GemmParams p) {
     constexpr int BM = WM * 32 * TM;
     constexpr int BN = WN * 32 * TN;
@@ -174,51 +171,11 @@ __global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[tm][tn][i] = 0.f;
 
-    // row-LayerNorm prologue (LNA): [mean | rstd] of the tile's BM rows, then [ln_w | ln_b]
-    __shared__ __attribute__((aligned(16))) float lnp[LNA ? 2 * BM + 2 * kLnMaxK : 4];
-    float ln_mean[TM], ln_rstd[TM];
-    if constexpr (LNA) {
-        for (int i = tid; i < p.K; i += 256) {
-            lnp[2 * BM + i] = p.ln_w[i];
-            lnp[2 * BM + kLnMaxK + i] = p.ln_b[i];
-        }
-        constexpr int PL = kLnMaxK / 64;
-        for (int rr = wave; rr < BM; rr += 4) {
-            const float* arow = A + (int64_t)min(m0 + rr, p.M - 1) * p.lda;
-            float v[PL];
-            float sum = 0.f;
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const int c = i * 64 + lane;
-                v[i] = c < p.K ? arow[c] : 0.f;
-                sum += v[i];
-            }
-            const float mean = wave_sum(sum) / (float)p.K;
-            float q = 0.f;
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const float d = (i * 64 + lane < p.K) ? v[i] - mean : 0.f;
-                q += d * d;
-            }
-            const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)p.K + p.ln_eps);
-            if (lane == 0) {
-                lnp[rr] = mean;
-                lnp[BM + rr] = rstd;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-            ln_mean[tm] = lnp[wr * 32 * TM + tm * 32 + r];
-            ln_rstd[tm] = lnp[BM + wr * 32 * TM + tm * 32 + r];
-        }
-    }
-
     const int fr = a_swz(r);
     // One stage = two MFMA k-steps.  All fragment reads of the stage are issued first, then
     // step 0's A fragments are split and its MFMAs issued; step 1's split is independent VALU
     // work the scheduler places in the shadow of step 0's MFMAs.
-    auto compute = [&](const char* abuf, const char* wbuf, int kt) {
+    auto compute = [&](const char* abuf, const char* wbuf) {
         float4 xa[2][TM][2];
         bf16x8 fw[2][P][TN];
 #pragma unroll
@@ -236,31 +193,6 @@ __global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm
                 for (int pl = 0; pl < P; ++pl)
                     fw[s][pl][tn] = *reinterpret_cast<const bf16x8*>(
                         wbuf + (((wc * TN + tn) * 2 + s) * P + pl) * 1024 + lane * 16);
-        }
-        if constexpr (LNA) {
-            // x' = (x - mean) * rstd * w[k] + b[k], the LN kernel's operation order
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int kb = kt * BK + 16 * s + 8 * h;
-                const float4 w0 = *reinterpret_cast<const float4*>(lnp + 2 * BM + kb);
-                const float4 w1 = *reinterpret_cast<const float4*>(lnp + 2 * BM + kb + 4);
-                const float4 b0 = *reinterpret_cast<const float4*>(lnp + 2 * BM + kLnMaxK + kb);
-                const float4 b1 = *reinterpret_cast<const float4*>(lnp + 2 * BM + kLnMaxK + kb + 4);
-#pragma unroll
-                for (int tm = 0; tm < TM; ++tm) {
-                    const float mu = ln_mean[tm], rs = ln_rstd[tm];
-                    float4& x0 = xa[s][tm][0];
-                    float4& x1 = xa[s][tm][1];
-                    x0.x = __builtin_fmaf((x0.x - mu) * rs, w0.x, b0.x);
-                    x0.y = __builtin_fmaf((x0.y - mu) * rs, w0.y, b0.y);
-                    x0.z = __builtin_fmaf((x0.z - mu) * rs, w0.z, b0.z);
-                    x0.w = __builtin_fmaf((x0.w - mu) * rs, w0.w, b0.w);
-                    x1.x = __builtin_fmaf((x1.x - mu) * rs, w1.x, b1.x);
-                    x1.y = __builtin_fmaf((x1.y - mu) * rs, w1.y, b1.y);
-                    x1.z = __builtin_fmaf((x1.z - mu) * rs, w1.z, b1.z);
-                    x1.w = __builtin_fmaf((x1.w - mu) * rs, w1.w, b1.w);
-                }
-            }
         }
         bf16x8 fa[2][P][TM];
         auto split_step = [&](int s) {
@@ -346,7 +278,7 @@ __global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm
         char* nb = slot(std::integral_constant<int, NEXT>());
         issue(min(kt + RING - 1, nk - 1), nb, nb + A_BYTES);
         char* cb = slot(Ic);
-        compute(cb, cb + A_BYTES, kt);
+        compute(cb, cb + A_BYTES);
     };
 
     issue(0, s0, s0 + A_BYTES);
@@ -392,22 +324,6 @@ int launch_cfg(const GemmParams& p, int batch, int epi, hipStream_t s) {
     dim3 grid(tiles, batch);
     dim3 block(256);
 #define VASR_L(E) hipLaunchKernelGGL((gemm_x3_kernel<WM, WN, TM, TN, RING, E, P>), grid, block, 0, s, p)
-#define VASR_LN(E) hipLaunchKernelGGL((gemm_x3_kernel<WM, WN, TM, TN, RING, E, P, true>), grid, block, 0, s, p)
-    if (p.ln_w) {
-        // the LN tables (4 KiB) do not fit beside two 80-KiB 128 x 128 rings: pick_x3 avoids it
-        if constexpr (BM * BN >= 128 * 128) {
-            set_error("vasr_linear_x3_f32: row LayerNorm not instantiated for the 128 x 128 tile");
-            return VASR_EINVAL;
-        } else switch (epi) {
-            case VASR_EPI_NONE: VASR_LN(VASR_EPI_NONE); break;
-            case VASR_EPI_GELU: VASR_LN(VASR_EPI_GELU); break;
-            case VASR_EPI_RESIDUAL: VASR_LN(VASR_EPI_RESIDUAL); break;
-            case VASR_EPI_ARGMAX: VASR_LN(VASR_EPI_ARGMAX); break;
-            default: set_error("vasr_linear_x3_f32: row LayerNorm with epilogue %d not supported", epi); return VASR_EINVAL;
-        }
-        return launch_status("vasr_linear_x3_f32");
-    }
-#undef VASR_LN
     switch (epi) {
         case VASR_EPI_NONE: VASR_L(VASR_EPI_NONE); break;
         case VASR_EPI_GELU: VASR_L(VASR_EPI_GELU); break;
@@ -460,8 +376,8 @@ static long x3_min_tiles(int cfg) {
     return cfg == 0 ? 19L * kCUs / 10 : 14L * kCUs / 10;
 }
 
-int pick_x3(int M, int N, int batch, bool pair, bool ln = false) {
-    for (int i = ln ? 1 : 0; i < 2; ++i) {
+int pick_x3(int M, int N, int batch, bool pair) {
+    for (int i = 0; i < 2; ++i) {
         const TileCfg& c = kCfgs[i];
         const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
         const bool exact_n = N % c.bn() == 0 || N > 4 * c.bn();  // little padding waste
@@ -549,14 +465,10 @@ VASR_API int vasr_linear_x3_f32(const vasr_gemm_args* a, const uint16_t* w_split
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     hipStream_t s = as_stream(stream);
-    if (epi != VASR_EPI_PAIR_POWER && epi != VASR_EPI_PAIR_FUSION && !p.ln_w) {
-        int rc;
-        if (try_panel_x3(p, epi, s, &rc)) return rc;
-    }
 #ifdef VASR_X3_FORCE_CFG
     const int cfg = VASR_X3_FORCE_CFG;  // diagnostic builds only
 #else
-    const int cfg = pick_x3(a->M, a->N, a->batch, pair, a->ln_w != nullptr);
+    const int cfg = pick_x3(a->M, a->N, a->batch, pair);
 #endif
     switch (cfg) {
         case 0: return launch_cfg<2, 2, 2, 2, RING_BIG, 3>(p, a->batch, epi, s);
@@ -598,7 +510,7 @@ VASR_API int vasr_linear_bf16(const vasr_gemm_args* a, const uint16_t* w_packed,
 #ifdef VASR_BF16_FORCE_CFG
     const int cfg = VASR_BF16_FORCE_CFG;  // diagnostic builds only
 #else
-    const int cfg = pick_x3(a->M, a->N, a->batch, pair, a->ln_w != nullptr);
+    const int cfg = pick_x3(a->M, a->N, a->batch, pair);
 #endif
     switch (cfg) {
         case 0: return launch_cfg<2, 2, 2, 2, RING_B16, 1>(p, a->batch, epi, s);

@@ -240,6 +240,23 @@ __global__ __launch_bounds__(256) void mel_chunk_norm_kernel(const float* __rest
         const float x = tb[i];
         dst[i] = i >= nv * n_mels ? 0.0f : normalize ? (x - st_s[2 * m]) / st_s[2 * m + 1] : x;
     }
+    // the zero frames of a padded layout: [0, frame_off) by the first chunk, [frame_off + F,
+    // out_stride / n_mels) by the last (the temporal conv's zero padding, no separate pass)
+    float* ob = out + (int64_t)b * out_stride;
+    if (c == 0)
+        for (int i = threadIdx.x; i < frame_off * n_mels; i += blockDim.x) ob[i] = 0.0f;
+    if (c == gridDim.x - 1) {
+        const int64_t lo = (int64_t)(frame_off + F) * n_mels, hi = out_stride / n_mels * n_mels;
+        for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) ob[i] = 0.0f;
+    }
+}
+
+// The same zero frames for the unchunked path (n_mels > kMaxMels or wide power rows).
+__global__ void zero_frames_kernel(float* __restrict__ out, int64_t out_stride, int frame_off, int F, int n_mels) {
+    float* ob = out + (int64_t)blockIdx.x * out_stride;
+    const int64_t lo = (int64_t)(frame_off + F) * n_mels, hi = out_stride / n_mels * n_mels;
+    for (int64_t i = threadIdx.x; i < hi; i += blockDim.x)
+        if (i < (int64_t)frame_off * n_mels || i >= lo) ob[i] = 0.0f;
 }
 
 __global__ void pad_frames_kernel(const float* __restrict__ x, float* __restrict__ out, int out_frames, int off,
@@ -255,8 +272,8 @@ __global__ void pad_frames_kernel(const float* __restrict__ x, float* __restrict
 
 }  // namespace
 
-// Stats + normalisation passes of the chunked front end over the workspace written by a
-// chunk-log pass (mel_chunk_log_kernel, or the fused STFT + log-mel of stft.hip).
+// Stats + normalisation passes of the chunked front end over the workspace written by the
+// chunk-log pass (mel_chunk_log_kernel).
 int mel_chunk_finish(float* workspace, float* out, int64_t out_stride, int frame_off, int B, int F, int n_mels,
                      int normalize, hipStream_t s, const int32_t* frames) {
     const int nch = (F + kFC - 1) / kFC;
@@ -317,6 +334,9 @@ static int mel_log_norm(const float* power, int64_t ld_power, int64_t stride_pow
     if (rc) return rc;
     hipLaunchKernelGGL(mel_norm_kernel, dim3((n_mels + 15) / 16, B), dim3(256), 0, s, workspace, out, out_stride,
                        frame_off, F, n_mels, normalize);
+    rc = launch_status(who);
+    if (rc || (frame_off == 0 && out_stride / n_mels == F)) return rc;
+    hipLaunchKernelGGL(zero_frames_kernel, dim3(B), dim3(256), 0, s, out, out_stride, frame_off, F, n_mels);
     return launch_status(who);
 }
 

@@ -244,9 +244,8 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
     // But its extra VALU issue slows the other utterance group's concurrent GEMMs: end to end
     // C2 +1.3 %, C3 (bf16) -2.6 %, C4 (30 s) -8.5 % (profiles/r02_npl/).  So 2 per lane is kept
     // for launches under half a wave per SIMD (B <= 4 at Di 384, N 64: 62 vs 69 us), where the
-    // shorter serial chain per wave wins.  VASR_SCAN_NPL=2|4 forces one.
-    const char* npl_s = std::getenv("VASR_SCAN_NPL");  // read per call (tests switch it)
-    const int npl_env = npl_s ? std::atoi(npl_s) : 0;
+    // shorter serial chain per wave wins.  vasr_set_option(VASR_OPT_SCAN_LANES, 2|4) (env VASR_SCAN_NPL) forces one.
+    const int npl_env = option(VASR_OPT_SCAN_LANES);  // vasr_set_option / env VASR_SCAN_NPL
     const long waves4 = (long)B * Di * N / 256;
     const bool two = npl_env == 2 || (npl_env != 4 && waves4 < 512);
 #define VASR_SCAN_N(NS, NN)                                                                                   \
@@ -295,10 +294,9 @@ VASR_API int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const flo
     hipStream_t s = as_stream(stream);
     // lane layout: 4 state indices per lane (the chunk-parallel grid has waves enough; 2 per lane
     // measured slower: 40.0 vs 35.9 us at B = 1, L = 501 and 43.4 vs 37.7 at L = 1501);
-    // VASR_SCAN_NPL=2 forces the other (outputs are bitwise those of the streaming kernel with
+    // VASR_OPT_SCAN_LANES = 2 forces the other (outputs are bitwise those of the streaming kernel with
     // the same layout; the layouts differ in the order of the y = sum_n h C partial sums)
-    const char* npl_s = std::getenv("VASR_SCAN_NPL");
-    const bool two = npl_s && std::atoi(npl_s) == 2;
+    const bool two = option(VASR_OPT_SCAN_LANES) == 2;
 #define VASR_SCAN_C(NS, NN)                                                                                         \
     (mode == 0 ? NS::launch_chunked_n<NN, 0>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, ws_a,   \
                                              ws_b, s)                                                             \

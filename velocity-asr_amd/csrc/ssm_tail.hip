@@ -313,10 +313,10 @@ __global__ void pack_weights16_kernel(const uint16_t* __restrict__ W, int64_t ld
 // 32 rows whatever M is, 21 us at 16), so 16-row blocks win while they still fit one per CU
 // (M <= 4096: the global-context blocks, one utterance at a time); above that two 16-row blocks
 // per CU duplicate the per-CU L2 -> VGPR weight stream: 33.2 vs 28.3 us at M = 8016,
-// 135.5k vs 136.1k RTFx end to end (profiles/r02e/tail_rows.txt).  VASR_TAIL_ROWS=16|32 forces
-// one (read per call).
+// 135.5k vs 136.1k RTFx end to end (profiles/r02e/tail_rows.txt).  vasr_set_option(VASR_OPT_TAIL_ROWS,
+// 16|32) (env VASR_TAIL_ROWS) forces one.
 int tail_rows(int M) {
-    if (const char* e = std::getenv("VASR_TAIL_ROWS")) return std::atoi(e) == 16 ? 16 : 32;
+    if (const int r = option(VASR_OPT_TAIL_ROWS)) return r;
     return M <= 4096 ? 16 : 32;  // 256 CUs x 16 rows
 }
 

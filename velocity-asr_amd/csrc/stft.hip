@@ -102,33 +102,16 @@ __device__ __forceinline__ void dft5(cf (&v)[5]) {
     v[3] = p2 + mul_pi(q2);
 }
 
-// FPB frames per workgroup.  MEL = false: |X|^2 rows to `power` (FPB = 6).  MEL = true (FPB =
-// kFC = 16, one log-mel chunk): the power rows stay in LDS and the chunk's log-mel rows and
-// fp64 (sum, sum of squares) partials are written exactly as mel_chunk_log_kernel writes them
-// (mel.hip), so the two-kernel and the fused front end agree bit for bit.
-struct MelArgs {
-    const int32_t* rowptr;
-    const int32_t* col;
-    const float* val;
-    float* tmp;     // (B, F, n_mels) log-mel rows
-    double* part;   // (B, nch, n_mels, 2) fp64 partials
-    int n_mels;
-};
-constexpr int kMelMaxNnz = 1024, kMelMaxBins = 85;
-
-template <int FPB, bool MEL>
+// FPB frames per workgroup, |X|^2 rows to `power`.
+template <int FPB>
 __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __restrict__ audio, int64_t ld_audio,
                                                              int S, const int32_t* __restrict__ samples, int F,
                                                              const float* __restrict__ window,
                                                              float* __restrict__ power, int64_t ldp,
-                                                             int64_t stridep, MelArgs ma) {
+                                                             int64_t stridep) {
     __shared__ cf tw[kHalf + kBins];  // W200^j, then W400^k
     __shared__ cf za[FPB][kHalf];
     __shared__ cf zb[FPB][kHalf];
-    __shared__ int rp_s[MEL ? kMelMaxBins + 1 : 1];
-    __shared__ int col_s[MEL ? kMelMaxNnz : 1];
-    __shared__ float val_s[MEL ? kMelMaxNnz : 1];
-    __shared__ float vals[MEL ? FPB * kMelMaxBins : 1];
     const int b = blockIdx.y, f0 = blockIdx.x * FPB;
     const int tid = threadIdx.x;
     const float* ab = audio + (int64_t)b * ld_audio;
@@ -160,17 +143,6 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
         x0[it] = ab[reflect(j0)];
         x1[it] = ab[reflect(j0 + 1)];
         w[it] = win2[n];
-    }
-    bool csr_lds = false;  // MEL: the CSR in LDS when it has <= kMelMaxNnz entries (393 for 80 x 201)
-    if constexpr (MEL) {
-        const int nnz = ma.rowptr[ma.n_mels];
-        csr_lds = nnz <= kMelMaxNnz;
-        for (int i = tid; i <= ma.n_mels; i += 256) rp_s[i] = ma.rowptr[i];
-        if (csr_lds)
-            for (int i = tid; i < nnz; i += 256) {
-                col_s[i] = ma.col[i];
-                val_s[i] = ma.val[i];
-            }
     }
 #pragma unroll
     for (int it = 0; it < kTwIt; ++it)
@@ -218,12 +190,11 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     // 6. real-FFT unpack by bin pairs (k, 200 - k), k = 0..100: with A, B the even / odd spectra
     //    at k, X[k] = A + W400^k B and X[200 - k] = conj(A - W400^k B).  |X|^2 is formed as
     //    re^2 + im^2 (the reference rounds through abs(): at most 1 ulp apart).
-    float* pw = reinterpret_cast<float*>(&za[0][0]);  // MEL: power rows [FPB][kBins] (za is free)
-    float* pb = MEL ? pw : power + (int64_t)b * stridep + (int64_t)f0 * ldp;  // uniform base
-    const int ldp32 = MEL ? kBins : (int)ldp;
+    float* pb = power + (int64_t)b * stridep + (int64_t)f0 * ldp;  // uniform base
+    const int ldp32 = (int)ldp;
     for (int i = tid; i < FPB * 101; i += 256) {
         const int q = i / 101, k = i - q * 101;
-        if (!MEL && f0 + q >= F) continue;
+        if (f0 + q >= F) continue;
         const cf zk = zb[q][k];
         const cf zm = zb[q][k == 0 ? 0 : kHalf - k];
         const cf zc = cf{zm.x, -zm.y};
@@ -233,37 +204,6 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
         float* row = pb + q * ldp32;
         row[k] = X1.x * X1.x + X1.y * X1.y;
         row[kHalf - k] = X2.x * X2.x + X2.y * X2.y;
-    }
-    if constexpr (MEL) {
-        // 7. log-mel of the chunk and its fp64 partials (mel_chunk_log_kernel's arithmetic)
-        __syncthreads();
-        const int n_mels = ma.n_mels, nch = gridDim.x;
-        const int nf = min(FPB, F - f0);
-        float* tb = ma.tmp + ((int64_t)b * F + f0) * n_mels;
-        for (int i = tid; i < nf * n_mels; i += 256) {
-            const int fl = i / n_mels, m = i - fl * n_mels;
-            const float* prow = pw + fl * kBins;
-            float acc = 0.f;
-            if (csr_lds)
-                for (int e = rp_s[m]; e < rp_s[m + 1]; ++e) acc = __builtin_fmaf(val_s[e], prow[col_s[e]], acc);
-            else
-                for (int e = rp_s[m]; e < rp_s[m + 1]; ++e) acc = __builtin_fmaf(ma.val[e], prow[ma.col[e]], acc);
-            const float v = logf(acc + 1e-10f);
-            vals[i] = v;
-            tb[i] = v;
-        }
-        __syncthreads();
-        for (int m = tid; m < n_mels; m += 256) {
-            double Ssum = 0.0, Q = 0.0;
-            for (int fl = 0; fl < nf; ++fl) {
-                const double v = (double)vals[fl * n_mels + m];
-                Ssum += v;
-                Q += v * v;
-            }
-            double* pp = ma.part + (((int64_t)b * nch + blockIdx.x) * n_mels + m) * 2;
-            pp[0] = Ssum;
-            pp[1] = Q;
-        }
     }
 }
 
@@ -280,8 +220,8 @@ static int stft_power_400(const float* audio, int64_t ld_audio, int B, int S, co
     const int F = (S + 2 * (kNfft / 2) - kNfft) / kHop + 1;
     VASR_CHECK_ARG(stride_power >= (int64_t)F * ldp, "%s: stride_power too small", who);
     if (B == 0) return VASR_OK;
-    hipLaunchKernelGGL((stft_power_400_kernel<kFPB, false>), dim3((F + kFPB - 1) / kFPB, B), dim3(256), 0,
-                       as_stream(stream), audio, ld_audio, S, samples, F, window, power, ldp, stride_power, MelArgs{});
+    hipLaunchKernelGGL((stft_power_400_kernel<kFPB>), dim3((F + kFPB - 1) / kFPB, B), dim3(256), 0,
+                       as_stream(stream), audio, ld_audio, S, samples, F, window, power, ldp, stride_power);
     return launch_status(who);
 }
 
@@ -300,29 +240,4 @@ VASR_API int vasr_stft_power_400_var_f32(const float* audio, int64_t ld_audio, i
     VASR_CHECK_ARG(samples, "vasr_stft_power_400_var_f32: null samples");
     return stft_power_400(audio, ld_audio, B, S, samples, window, power, ldp, stride_power, stream,
                           "vasr_stft_power_400_var_f32");
-}
-
-VASR_API int vasr_stft_logmel_400_f32(const float* audio, int64_t ld_audio, int B, int S, const float* window,
-                                      const int32_t* fb_rowptr, const int32_t* fb_col, const float* fb_val,
-                                      float* out, int64_t out_stride, int frame_off, int n_mels, int normalize,
-                                      float* workspace, void* stream) {
-    using namespace vasr;
-    VASR_CHECK_ARG(audio && window && fb_rowptr && fb_col && fb_val && out && workspace,
-                   "vasr_stft_logmel_400_f32: null pointer");
-    VASR_CHECK_ARG(((uintptr_t)window & 7) == 0, "vasr_stft_logmel_400_f32: window must be 8-byte aligned");
-    VASR_CHECK_ARG(B >= 0 && S > kNfft / 2 && ld_audio >= S && n_mels >= 1 && n_mels <= kMelMaxBins && frame_off >= 0,
-                   "vasr_stft_logmel_400_f32: bad shape (S=%d n_mels=%d)", S, n_mels);
-    const int F = (S + 2 * (kNfft / 2) - kNfft) / kHop + 1;
-    VASR_CHECK_ARG(out_stride >= (int64_t)(F + frame_off) * n_mels, "vasr_stft_logmel_400_f32: out_stride too small");
-    if (B == 0) return VASR_OK;
-    static_assert(kMelChunk == 16, "one log-mel chunk per workgroup");
-    hipStream_t s = as_stream(stream);
-    const int nch = (F + kMelChunk - 1) / kMelChunk;
-    MelArgs ma{fb_rowptr, fb_col, fb_val, workspace,
-               reinterpret_cast<double*>(workspace + (((int64_t)B * F * n_mels + 1) & ~(int64_t)1)), n_mels};
-    hipLaunchKernelGGL((stft_power_400_kernel<kMelChunk, true>), dim3(nch, B), dim3(256), 0, s, audio, ld_audio, S,
-                       nullptr, F, window, nullptr, 0, 0, ma);
-    const int rc = launch_status("vasr_stft_logmel_400_f32");
-    if (rc) return rc;
-    return mel_chunk_finish(workspace, out, out_stride, frame_off, B, F, n_mels, normalize, s);
 }

@@ -28,6 +28,9 @@ inline int launch_status(const char* what) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Current value of a vasr_set_option key (enum vasr_option); 0 = automatic.
+int option(int key);
+
 // mel.hip: the stats + normalisation passes of the chunked log-mel front end (kFC = 16 frames
 // per chunk) over a workspace laid out as vasr_mel_workspace_floats describes.
 constexpr int kMelChunk = 16;

@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -23,6 +23,7 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "vasr.
 
 (EPI_NONE, EPI_GELU, EPI_SOFTPLUS_FROM, EPI_RESIDUAL, EPI_GELU_PE, EPI_PAIR_POWER, EPI_PAIR_FUSION,
  EPI_ARGMAX) = range(8)
+OPT_SCAN_LANES, OPT_SCAN_CHUNK, OPT_TAIL_ROWS = range(3)  # enum vasr_option
 
 c_i32, c_i64, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -41,14 +42,13 @@ class GemmArgs(ctypes.Structure):
         ("aux2", c_p),
         ("n_out", c_i32),
         ("qparams", c_p),
-        ("ln_w", c_p), ("ln_b", c_p), ("ln_eps", ctypes.c_float),
     ]
 
 
 _SIGNATURES = {
     "vasr_version": ([], ctypes.c_int),
+    "vasr_set_option": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "vasr_last_error": ([], ctypes.c_char_p),
-    "vasr_linear_f32": ([ctypes.POINTER(GemmArgs), c_p], ctypes.c_int),
     "vasr_linear_x3_f32": ([ctypes.POINTER(GemmArgs), c_p, c_p], ctypes.c_int),
     "vasr_split_weights_bf16x3": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
     "vasr_split_weights_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
@@ -65,11 +65,6 @@ _SIGNATURES = {
     "vasr_ssm_scan_workspace_floats": ([ctypes.c_int] * 4, c_i64),
     "vasr_ssm_block_tail_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                 + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
-    "vasr_stream_create_cu_mask": ([c_p, ctypes.c_int, c_p], ctypes.c_int),
-    "vasr_stream_destroy": ([c_p], ctypes.c_int),
-    "vasr_device_cu_count": ([], ctypes.c_int),
-    "vasr_ssm_block_head_f32": ([c_p, c_i64, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, ctypes.c_int, c_p, c_i64, c_p,
-                                 c_i64] + [ctypes.c_int] * 6 + [c_p], ctypes.c_int),
     "vasr_ssm_block_tail_bf16": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                  + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_pack_weights16_bf16": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
@@ -83,9 +78,6 @@ _SIGNATURES = {
     "vasr_mel_log_norm_f32": ([c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p, c_p],
                               ctypes.c_int),
     "vasr_mel_workspace_floats": ([ctypes.c_int] * 3, c_i64),
-    "vasr_set_x3_engine": ([ctypes.c_int], ctypes.c_int),
-    "vasr_stft_logmel_400_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 3
-                                 + [c_p, c_p], ctypes.c_int),
     "vasr_stft_power_400_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_i64, c_i64, c_p], ctypes.c_int),
     "vasr_stft_power_400_var_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p, c_i64, c_i64, c_p],
                                     ctypes.c_int),

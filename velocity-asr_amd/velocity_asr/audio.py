@@ -262,11 +262,8 @@ def compute_mel_spectrogram(audio: torch.Tensor, sample_rate: int = SAMPLE_RATE,
 
 
 # Default geometry (n_fft 400, hop 160): the real-FFT launch writing |X|^2 rows (6 frames per
-# workgroup), then the chunked log-mel passes.  VASR_STFT=fused: FFT + log-mel chunk pass in one
-# launch (vasr_stft_logmel_400_f32, 16 frames per workgroup, power kept in LDS; bit-identical,
-# but measured slower: 39.9 vs 35.4 us per 16-clip launch, the larger workgroups hide less
-# latency).  VASR_STFT=gemm or other geometries: reflect pad + windowed-DFT GEMM with the |X|^2
-# epilogue.
+# workgroup), then the chunked log-mel passes.  VASR_STFT=gemm or other geometries: reflect pad
+# + windowed-DFT GEMM with the |X|^2 epilogue.
 _STFT_MODE = os.environ.get("VASR_STFT", "fft")
 _STFT_FFT = _STFT_MODE != "gemm"
 
@@ -280,13 +277,17 @@ def ragged_supported(n_mels: int = N_MELS, n_fft: int = N_FFT, hop_length: int =
 
 def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = N_FFT,
                   hop_length: int = HOP_LENGTH, n_mels: int = N_MELS, normalize: bool = True,
-                  lengths=None) -> torch.Tensor:
+                  lengths=None, frame_pad: int = 0) -> torch.Tensor:
     """(B, S) float32 HIP tensor -> (B, F, n_mels) on the same device.
 
     lengths (extension): per-utterance sample counts of a batch of clips of different lengths,
     zero-padded to S.  Utterance b's first audio_to_frames(lengths[b]) frames are then those of
     the clip alone (its reflect padding and its normalisation statistics are its own) and its
-    later frames are 0; pass the frame counts on as VELOCITYASR(..., frames=)."""
+    later frames are 0; pass the frame counts on as VELOCITYASR(..., frames=).
+
+    frame_pad (extension): write the mel into a buffer with frame_pad zero frames before and
+    after each utterance (the normalisation pass writes them) and return the (B, F, n_mels)
+    view into it: the temporal conv (padding 1) then reads it in place, with no padding pass."""
     B, S = x.shape
     pad = n_fft // 2
     if S <= pad:
@@ -306,18 +307,18 @@ def mel_on_device(x: torch.Tensor, sample_rate: int = SAMPLE_RATE, n_fft: int = 
         frames = torch.tensor([(v + 2 * pad - n_fft) // hop_length + 1 for v in lengths], dtype=torch.int32).to(x.device)
         power = ops.stft_power_400(x, tb.window, samples=samples)
         return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize,
-                                frames=frames)
+                                frames=frames, frame_pad=frame_pad)
     if n_fft == 400 and hop_length == 160 and _STFT_FFT:
-        if _STFT_MODE == "fused" and n_mels <= 85:  # FFT + log-mel in one launch (power stays in LDS)
-            return ops.stft_logmel_400(x, tb.window, tb.fb_csr, n_mels, normalize)
         power = ops.stft_power_400(x, tb.window)
-        return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize)
+        return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize,
+                                frame_pad=frame_pad)
     ld = (S + 2 * pad + 3) // 4 * 4
     xp = ops.reflect_pad(x, pad, ld)
     power = torch.empty((B, n_frames, tb.n_bins), device=x.device, dtype=torch.float32)
     ops.gemm_batched(xp, hop_length, ld, n_frames, B, n_fft, tb.dft, None, power, tb.n_bins, n_frames * tb.n_bins,
                      epilogue=_lib.EPI_PAIR_POWER, n_out=tb.n_bins)
-    return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize)
+    return ops.mel_log_norm(power, tb.n_bins, n_frames * tb.n_bins, tb.fb_csr, B, n_frames, n_mels, normalize,
+                            frame_pad=frame_pad)
 
 
 class MelSpectrogramTransform(nn.Module):

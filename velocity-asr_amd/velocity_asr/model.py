@@ -95,6 +95,9 @@ class TemporalBindingLayer(nn.Module):
         self.norm = nn.LayerNorm(d_model)
         self.activation = nn.GELU()
 
+    def conv_padding(self) -> int:
+        return Q.inner(self.conv).padding[0]
+
     def output_length(self, frames: int) -> int:
         c = Q.inner(self.conv)
         k, s, p = c.kernel_size[0], c.stride[0], c.padding[0]

@@ -107,25 +107,23 @@ def _rows(name: str, t: torch.Tensor) -> Tuple[int, int, int]:
     return t.shape[0], t.shape[1], t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
 
 
-# GEMM engine: "x3" = fp32 GEMM as split-bf16 products on the bf16 matrix cores
-# (vasr_linear_x3_f32, fp32-accurate, 2.67x the f32-MFMA rate); "f32" = f32-input MFMA.
-_GEMM_MODES = ("x3", "f32")
-_gemm_mode = os.environ.get("VASR_GEMM", "x3")
-if _gemm_mode not in _GEMM_MODES:
-    raise ValueError(f"VASR_GEMM={_gemm_mode!r}: expected one of {_GEMM_MODES}")
+class option:
+    """Set a launcher tuning option (vasr_set_option; enum vasr_option in include/vasr.h) for the
+    duration of a with-block, e.g. ``with ops.option(L.OPT_SCAN_CHUNK, 16): ...``.  Options
+    change work decomposition only, never the computed values."""
 
+    def __init__(self, key: int, value: int):
+        self.key, self.value = key, value
 
-def gemm_mode() -> str:
-    return _gemm_mode
+    def __enter__(self):
+        prev = L.lib().vasr_set_option(self.key, self.value)
+        check(min(prev, 0), "vasr_set_option")
+        self.prev = prev
+        return self
 
-
-def set_gemm_mode(mode: str) -> str:
-    """Select the GEMM engine; returns the previous mode."""
-    global _gemm_mode
-    if mode not in _GEMM_MODES:
-        raise ValueError(f"gemm mode {mode!r}: expected one of {_GEMM_MODES}")
-    prev, _gemm_mode = _gemm_mode, mode
-    return prev
+    def __exit__(self, *exc):
+        L.lib().vasr_set_option(self.key, self.prev)
+        return False
 
 
 # Split-bf16 planes of weight matrices, built once per (tensor, version) and dropped with the
@@ -215,34 +213,6 @@ def ssm_block_tail(g: torch.Tensor, x: torch.Tensor, wo: torch.Tensor, ln_w: tor
     return out
 
 
-def ssm_block_head(x: torch.Tensor, B: int, Lq: int, ln_w, ln_b, ln_eps: float, conv_w, conv_b, w_in: torch.Tensor,
-                   w_xdt: torch.Tensor, b_xdt: torch.Tensor, n_sp: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Fused SSMBlock head (vasr_ssm_block_head_f32): LN1 + causal dwconv -> in_proj -> [x_proj;
-    dt_proj] (+bias, softplus from column n_sp).  x (B*L, 192) -> (xz (B*L, 768), xdt (B*L, 512))."""
-    bf16 = w_in.dtype == torch.bfloat16
-    ln_w, ln_b, conv_w, conv_b, b_xdt = f32(ln_w), f32(ln_b), f32(conv_w), f32(conv_b), f32(b_xdt)
-    for n, t in (("x", x), ("ln_w", ln_w), ("ln_b", ln_b), ("conv_w", conv_w), ("conv_b", conv_b), ("b_xdt", b_xdt)):
-        _cuda_f32(f"ssm_block_head.{n}", t)
-    if bf16 != (w_xdt.dtype == torch.bfloat16):
-        raise TypeError("ssm_block_head: mixed weight dtypes")
-    M, D, ldx = _rows("ssm_block_head.x", x)
-    E2, Dw = w_in.shape
-    Nx, Di = w_xdt.shape
-    if M != B * Lq or Dw != D or E2 != 2 * Di or b_xdt.numel() != Nx:
-        raise ValueError("ssm_block_head: inconsistent shapes")
-    prep = pack_weights16 if bf16 else split_weights16
-    xz = torch.empty((M, E2), device=x.device, dtype=torch.float32)
-    xdt = torch.empty((M, Nx), device=x.device, dtype=torch.float32)
-    ev = _t0("ssm_head")
-    check(L.lib().vasr_ssm_block_head_f32(x.data_ptr(), ldx, ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(),
-                                          float(ln_eps), conv_w.contiguous().data_ptr(), conv_b.contiguous().data_ptr(),
-                                          prep(w_in).data_ptr(), prep(w_xdt).data_ptr(), b_xdt.contiguous().data_ptr(),
-                                          int(n_sp), xz.data_ptr(), E2, xdt.data_ptr(), Nx, M, Lq, D, Di, Nx, int(bf16),
-                                          stream_of(x)), "vasr_ssm_block_head_f32")
-    _t1("ssm_head", ev, dict(M=M, D=D, Di=Di, Nx=Nx))
-    return xz, xdt
-
-
 def pack_bf16(w: torch.Tensor) -> torch.Tensor:
     """One fragment-native bf16 plane (as int16 storage) of a (N, K) bf16 weight view."""
     N, K, ldw = _rows("pack.w", w)
@@ -258,48 +228,22 @@ def pack_bf16(w: torch.Tensor) -> torch.Tensor:
     return packed
 
 
-def set_x3_engine(engine: str) -> str:
-    """Main loop of the split-bf16 GEMM: "tiles" (LDS-ring tiles, the default) or "panel" /
-    "panel2" (LDS-resident weight panels where the shape allows; experimental, bit-identical).
-    Returns the previous one."""
-    codes = {"tiles": 0, "panel": 1, "panel2": 2}  # panel2: the 2-waves-per-SIMD panel variant
-    if engine not in codes:
-        raise ValueError(f"x3 engine {engine!r}: expected one of {tuple(codes)}")
-    prev = L.lib().vasr_set_x3_engine(codes[engine])
-    return {v: k for k, v in codes.items()}[prev]
-
-
 def _linear(args: GemmArgs, w: torch.Tensor, stream) -> None:
     if w.dtype == torch.bfloat16:
         check(L.lib().vasr_linear_bf16(args, pack_bf16(w).data_ptr(), stream), "vasr_linear_bf16")
-    elif _gemm_mode == "x3":
-        check(L.lib().vasr_linear_x3_f32(args, split_weights(w).data_ptr(), stream), "vasr_linear_x3_f32")
     else:
-        check(L.lib().vasr_linear_f32(args, stream), "vasr_linear_f32")
+        check(L.lib().vasr_linear_x3_f32(args, split_weights(w).data_ptr(), stream), "vasr_linear_x3_f32")
 
 
-_LN_EPILOGUES = (L.EPI_NONE, L.EPI_GELU, L.EPI_RESIDUAL, L.EPI_ARGMAX)
-
-
-def _ln_prologue(a: torch.Tensor, w: torch.Tensor, ln, epilogue: int, args: GemmArgs):
-    """Row LayerNorm of `a`: by default vasr_layer_norm_f32 first; with VASR_LN_PROLOGUE=1 fused
-    into the GEMM's A read where the engine supports it (split-bf16 or bf16 engine, K % 32 == 0,
-    K <= 384, NONE / GELU / RESIDUAL / ARGMAX).  Both give identical results.  The fused form
-    is opt-in because it measured slower end to end (99.5k vs 102.5k RTFx): its per-block
-    statistics pass re-reads the A tile and delays the main loop by more than the separate
-    5-us LayerNorm launch costs, and the CTC head loses its 128 x 128 tile (LDS budget).
-    Returns the A the GEMM reads."""
+def _ln_prologue(a: torch.Tensor, ln) -> torch.Tensor:
+    """Row LayerNorm of `a` (vasr_layer_norm_f32) when ln = (weight, bias, eps) is given: the
+    LayerNorm feeding a Linear (SSMBlock norm2 -> FFN, the CTC head).  Returns the A the GEMM
+    reads.  (Fusing it into the GEMM's A read was bit-identical but slower end to end, 99.5k vs
+    102.5k RTFx; removed in r03)"""
     if ln is None:
         return a
     ln_w, ln_b, eps = ln
-    ln_w, ln_b = f32(ln_w), f32(ln_b)
-    K = a.shape[1]
-    fused = ((w.dtype == torch.bfloat16 or _gemm_mode == "x3") and epilogue in _LN_EPILOGUES
-             and K % 32 == 0 and K <= 384 and os.environ.get("VASR_LN_PROLOGUE", "0") == "1")
-    if not fused:
-        return layer_norm(a, ln_w, ln_b, eps)
-    args.ln_w, args.ln_b, args.ln_eps = ln_w.data_ptr(), ln_b.data_ptr(), float(eps)
-    return a
+    return layer_norm(a, f32(ln_w), f32(ln_b), eps)
 
 
 def _qp(qparams: Optional[torch.Tensor], cols: int) -> Optional[int]:
@@ -317,10 +261,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
          qparams: Optional[torch.Tensor] = None, ln=None) -> torch.Tensor:
     """out = epilogue(fq(a @ w.T + bias)) for a (M, K) row view and w (N, K); fq is the
     per-column activation fake-quant of `qparams` ((ncols, 4) {scale, zp, qmin, qmax}) if given.
-    ln = (weight, bias, eps): LayerNorm each row of `a` first (fused into the A read)."""
+    ln = (weight, bias, eps): LayerNorm each row of `a` first."""
     _cuda_f32("gemm.a", a)
     args = GemmArgs()
-    a = _ln_prologue(a, w, ln, epilogue, args)
+    a = _ln_prologue(a, ln)
     _cuda_w("gemm.w", w)
     bias, aux, aux2 = f32(bias), f32(aux), f32(aux2)
     M, K, lda = _rows("gemm.a", a)
@@ -353,10 +297,10 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
                 qparams: Optional[torch.Tensor] = None, ln=None) -> torch.Tensor:
     """int32 argmax over the N outputs of a @ w.T + bias (after qparams) per row, fused into the
     GEMM epilogue (VASR_EPI_ARGMAX): the (M, N) product is never written.  Ties -> first index.
-    ln = (weight, bias, eps): LayerNorm each row of `a` first (fused into the A read)."""
+    ln = (weight, bias, eps): LayerNorm each row of `a` first."""
     _cuda_f32("gemm_argmax.a", a)
     args = GemmArgs()
-    a = _ln_prologue(a, w, ln, L.EPI_ARGMAX, args)
+    a = _ln_prologue(a, ln)
     _cuda_w("gemm_argmax.w", w)
     bias = f32(bias)
     M, K, lda = _rows("gemm_argmax.a", a)
@@ -458,16 +402,26 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
 # Chunk-parallel tree scan (vasr_ssm_scan_chunked_f32, bitwise equal to the streaming kernel)
 # for launches under CHUNKED_MAX_WAVES waves of the streaming kernel (B * Di * N / 256; 768 on
 # 1024 SIMDs): one utterance at a time, as the reference's scripts feed the model.
-# VASR_SCAN_CHUNKED=0|1 forces the streaming / chunked form (read per call).
+# scan_form("streaming" | "chunked" | None) forces one (default from VASR_SCAN_CHUNKED=0|1).
 CHUNKED_MAX_WAVES = 512
+_SCAN_FORM = {"0": "streaming", "1": "chunked"}.get(os.environ.get("VASR_SCAN_CHUNKED", ""))
+
+
+def scan_form(form: Optional[str]) -> Optional[str]:
+    """Force the streaming or chunk-parallel tree scan (None = by launch size); returns the
+    previous setting.  Both give bitwise equal outputs."""
+    global _SCAN_FORM
+    if form not in (None, "streaming", "chunked"):
+        raise ValueError(f"scan form {form!r}: expected None, 'streaming' or 'chunked'")
+    prev, _SCAN_FORM = _SCAN_FORM, form
+    return prev
 
 
 def _use_chunked(B: int, Lq: int, Di: int, N: int, mode: int) -> bool:
     if mode not in (0, 2) or Lq <= 16:
         return False
-    env = os.environ.get("VASR_SCAN_CHUNKED")
-    if env is not None:
-        return env == "1"
+    if _SCAN_FORM is not None:
+        return _SCAN_FORM == "chunked"
     return B * Di * N // 256 < CHUNKED_MAX_WAVES
 
 
@@ -548,41 +502,44 @@ def stft_power_400(audio: torch.Tensor, window: torch.Tensor, samples: Optional[
     return power
 
 
-def stft_logmel_400(audio: torch.Tensor, window: torch.Tensor, fb_csr, n_mels: int, normalize: bool) -> torch.Tensor:
-    """(B, S) audio -> (B, S // 160 + 1, n_mels) normalised log-mel (n_fft 400, hop 160): one fused
-    FFT + log-mel launch (power stays on chip) and the stats / normalisation passes."""
-    _cuda_f32("stft_logmel_400.audio", audio)
-    _cuda_f32("stft_logmel_400.window", window)
-    audio = audio.contiguous()
-    B, S = audio.shape
-    F = S // 160 + 1
-    rowptr, col, val = fb_csr
-    out = torch.empty((B, F, n_mels), device=audio.device, dtype=torch.float32)
-    ws = torch.empty(int(L.lib().vasr_mel_workspace_floats(B, F, n_mels)), device=audio.device, dtype=torch.float32)
-    check(L.lib().vasr_stft_logmel_400_f32(audio.data_ptr(), S, B, S, window.contiguous().data_ptr(), rowptr.data_ptr(),
-                                           col.data_ptr(), val.data_ptr(), out.data_ptr(), F * n_mels, 0, n_mels,
-                                           int(normalize), ws.data_ptr(), stream_of(audio)), "vasr_stft_logmel_400_f32")
-    return out
-
-
 def mel_log_norm(power: torch.Tensor, ld_power: int, stride_power: int, fb_csr, B: int, F: int, n_mels: int,
-                 normalize: bool, frames: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """frames: per-utterance frame counts (int32 (B,), each <= F); frames past them are 0."""
+                 normalize: bool, frames: Optional[torch.Tensor] = None, frame_pad: int = 0) -> torch.Tensor:
+    """frames: per-utterance frame counts (int32 (B,), each <= F); frames past them are 0.
+    frame_pad > 0: the mel is written into a (B, F + 2 frame_pad, n_mels) buffer whose outer
+    frames the kernel zero-fills, and the (B, F, n_mels) view into it is returned, marked as
+    zero-framed (zero_framed()) so the temporal conv reads it without a padding copy."""
     rowptr, col, val = fb_csr
-    out = torch.empty((B, F, n_mels), device=power.device, dtype=torch.float32)
+    Fo = F + 2 * frame_pad
+    buf = torch.empty((B, Fo, n_mels), device=power.device, dtype=torch.float32)
     ws = torch.empty(int(L.lib().vasr_mel_workspace_floats(B, F, n_mels)), device=power.device, dtype=torch.float32)
     frames = _lens("mel_log_norm.frames", frames, B, power.device)
     if frames is None:
         check(L.lib().vasr_mel_log_norm_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(),
-                                            col.data_ptr(), val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F,
-                                            n_mels, int(normalize), ws.data_ptr(), stream_of(power)),
+                                            col.data_ptr(), val.data_ptr(), buf.data_ptr(), Fo * n_mels, frame_pad, B,
+                                            F, n_mels, int(normalize), ws.data_ptr(), stream_of(power)),
               "vasr_mel_log_norm_f32")
     else:
         check(L.lib().vasr_mel_log_norm_var_f32(power.data_ptr(), ld_power, stride_power, rowptr.data_ptr(),
-                                                col.data_ptr(), val.data_ptr(), out.data_ptr(), F * n_mels, 0, B, F,
-                                                n_mels, int(normalize), frames.data_ptr(), ws.data_ptr(),
+                                                col.data_ptr(), val.data_ptr(), buf.data_ptr(), Fo * n_mels, frame_pad,
+                                                B, F, n_mels, int(normalize), frames.data_ptr(), ws.data_ptr(),
                                                 stream_of(power)), "vasr_mel_log_norm_var_f32")
+    if not frame_pad:
+        return buf
+    out = buf[:, frame_pad:frame_pad + F]
+    out._vasr_zero_framed = (buf, frame_pad)
     return out
+
+
+def zero_framed(x: torch.Tensor, pad: int):
+    """The (B, F + 2 q, C) buffer of a (B, F, C) view written by mel_log_norm(..., frame_pad=q)
+    with q >= pad zero frames on each side, sliced to `pad` zero frames, or None."""
+    ent = getattr(x, "_vasr_zero_framed", None)
+    if ent is None:
+        return None
+    buf, q = ent
+    if q < pad or buf.data_ptr() + q * buf.shape[2] * 4 != x.data_ptr() or x.shape[1] + 2 * q != buf.shape[1]:
+        return None
+    return buf[:, q - pad:q + x.shape[1] + pad]
 
 
 def pad_frames(x: torch.Tensor, out_frames: int, off: int) -> torch.Tensor:

@@ -261,9 +261,16 @@ def conv1d_rows(mod: nn.Module, x_frames: torch.Tensor, epilogue: int = _lib.EPI
         w = effective_weight(mod)                   # (D, C, k) -> (D, k*C), frame-major rows
         return w.permute(0, 2, 1).reshape(D, -1).contiguous()
     w = cached(mod, "wrows", (inner(mod).weight,) + _wq_deps(mod), wbuild)
-    buf = ops.pad_frames(x_frames, frames, p)
+    # a mel the device pipeline wrote zero-framed (ops.mel_log_norm(..., frame_pad)) is read in
+    # place: its batch stride is (Lin + 2 q) frames; else one padding copy
+    zf = ops.zero_framed(x_frames, p) if frames == Lin + 2 * p else None
+    if zf is not None:
+        buf, ld_b = zf, zf.stride(0)
+    else:
+        buf = ops.pad_frames(x_frames, frames, p)
+        ld_b = frames * C
     out = torch.empty((B, L, D), device=buf.device, dtype=torch.float32)
-    ops.gemm_batched(buf, s * C, frames * C, L, B, k * C, w, c.bias, out, D, L * D, epilogue=epilogue, aux=aux,
+    ops.gemm_batched(buf, s * C, ld_b, L, B, k * C, w, c.bias, out, D, L * D, epilogue=epilogue, aux=aux,
                      ld_aux=ld_aux, stride_aux=0, qparams=act_qparams(mod, D))
     return out
 

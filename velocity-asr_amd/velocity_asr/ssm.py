@@ -157,26 +157,14 @@ class SSMBlock(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def _fused_tail_ok(self, D: int) -> bool:
-        """The one-launch tail (vasr_ssm_block_tail_f32 / _bf16) serves the fp32 model (split-bf16
-        engine) and the bf16 model at d_model 192 / FFN width 384; VASR_FUSED_TAIL=0 selects the
-        launches below (read per call so tests can compare the two)."""
+        """The one-launch tail (vasr_ssm_block_tail_f32 / _bf16) serves the fp32 and the bf16
+        model at d_model 192 / FFN width 384; VASR_FUSED_TAIL=0 selects the launches below (read
+        per call so tests can compare the two)."""
         w = self.ffn[0].weight
-        dtype_ok = w.dtype == torch.bfloat16 or (w.dtype == torch.float32 and ops.gemm_mode() == "x3")
+        dtype_ok = w.dtype in (torch.bfloat16, torch.float32)
         return (os.environ.get("VASR_FUSED_TAIL", "1") != "0" and dtype_ok and D == 192
                 and tuple(w.shape) == (384, 192) and self.ssm.d_inner == 384
                 and self.ssm.out_proj.weight.dtype == w.dtype == self.ffn[3].weight.dtype)
-
-    def _fused_head_ok(self, D: int) -> bool:
-        """The one-launch head (vasr_ssm_block_head_f32: d_model 192, d_inner 384, state dim 64,
-        kernel 4) is opt-in (VASR_FUSED_HEAD=1): alone it matches the three launches (59.6 vs
-        62.2 us per 16-clip block) but end to end it is slower (119k vs 132k RTFx: one 108-KB-LDS
-        block per CU for its whole duration keeps the other stream's scan off those CUs), and at
-        B = 1 its 2 MB weight stream per 32-row block makes it slower alone too (49 vs 38 us)."""
-        w = self.ssm.in_proj.weight
-        dtype_ok = w.dtype == torch.bfloat16 or (w.dtype == torch.float32 and ops.gemm_mode() == "x3")
-        return (os.environ.get("VASR_FUSED_HEAD", "0") == "1" and dtype_ok and D == 192
-                and self.ssm.d_inner == 384 and self.ssm.state_dim == 64 and self.conv.kernel_size[0] == 4
-                and self.ssm.x_proj.weight.dtype == self.ssm.dt_proj.weight.dtype == w.dtype)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _check_eval(self)
@@ -195,16 +183,9 @@ class SSMBlock(nn.Module):
         B, L, D = x.shape
         x = x.contiguous()
         x2 = x.view(B * L, D)
-        if self._fused_head_ok(D):
-            # LN1 + causal dwconv -> in_proj -> [x_proj; dt_proj] + softplus in one kernel (u stays on chip)
-            p = self.ssm._prepared()
-            xz, xdt = ops.ssm_block_head(x2, B, L, self.norm1.weight, self.norm1.bias, self.norm1.eps,
-                                         ops.f32(self.conv.weight).view(D, -1), self.conv.bias,
-                                         self.ssm.in_proj.weight, p["w_xdt"], p["b_xdt"], 2 * self.ssm.state_dim)
-        else:
-            u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
-                              self.conv.bias, self.norm1.eps)
-            xz, xdt = self.ssm.project(u.view(B * L, D))
+        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
+                          self.conv.bias, self.norm1.eps)
+        xz, xdt = self.ssm.project(u.view(B * L, D))
         return x2, xz, xdt
 
     def tail(self, g: torch.Tensor, x2: torch.Tensor, B: int, L: int) -> torch.Tensor:

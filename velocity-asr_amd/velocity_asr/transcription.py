@@ -74,7 +74,8 @@ def _decode_batch(model, audio: torch.Tensor, decoder: CTCDecoder, timestamps: b
     """(b, S) device audio -> [(text, words or None)] through the device pipeline.  lengths:
     per-clip sample counts when the clips were zero-padded to S."""
     with torch.no_grad():
-        mel = mel_on_device(audio, n_mels=model.config.mel_bins, lengths=lengths)
+        mel = mel_on_device(audio, n_mels=model.config.mel_bins, lengths=lengths,
+                            frame_pad=model.temporal_binding.conv_padding())
         frames = None if lengths is None else [n // HOP_LENGTH + 1 for n in lengths]
         if beam_width > 1:
             logits = model(mel, frames=frames)
