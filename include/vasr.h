@@ -158,8 +158,12 @@ int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b,
  *          scan_mode="parallel", VASR_SCAN_FMA=0 selects mode 0);
  *   out[b,t,d] = (sum_n h[b,t,d,n] C[b,t,n] + x[b,t,d] D[d]) * silu(z[b,t,d]).
  * x = xz[:, :, 0:Di], z = xz[:, :, Di:2Di]; B = bc[:, :, 0:N], C = bc[:, :, N:2N].
- * A2 = A * log2(e) (A = -exp(A_log), shared across Di).  N in {16, 32, 64};
- * Di % (4096/N) == 0 for N = 64 ... (host checks); L <= 8192.
+ * A2 = A * log2(e) (A = -exp(A_log), shared across Di).  N in {16, 32, 64, 128}: any other
+ * state dim N' < 128 runs as the next size up with B and C zero-padded (columns N'..N-1 of each
+ * half of bc) and A2 padded with 0 -- the padded states then stay exactly 0 and add nothing to
+ * y, so the outputs are those of N' states (velocity_asr.ssm pads the projection weights with
+ * zero rows, so the GEMM writes that layout).  Di a multiple of 4 * 64 * NPL / N channels per
+ * workgroup (16 at N = 64, 8 at N = 128; host checks); L <= 8192.
  */
 int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,
                       const float* bc, int64_t ld_bc, const float* A2, const float* D,

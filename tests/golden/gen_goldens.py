@@ -532,6 +532,38 @@ def gen_benchsets():
     save("fwd_benchsets.npz", **out)
 
 
+STATEDIM_CFGS = {"sd8": dict(ssm_state_dim=8, global_ssm_state_dim=8),
+                 "sd48": dict(ssm_state_dim=48, global_ssm_state_dim=24),
+                 "sd128": dict(ssm_state_dim=128, global_ssm_state_dim=128)}
+STATEDIM_SCANS = [("N8", 120, 2, 100, 16, 8), ("N48", 121, 1, 257, 16, 48), ("N128", 122, 2, 301, 8, 128)]
+
+
+def gen_statedims():
+    """State dims the scan kernels are not built for: SelectiveSSM(state_dim)
+    and VelocityASRConfig.ssm_state_dim / global_ssm_state_dim take any N (ssm.py:32-90,
+    model.py:23-68).  Whole-model forwards at N = 8, 48, 128 and scans at the same N."""
+    out = {}
+    for name, cfg in STATEDIM_CFGS.items():
+        model = build_model(cfg, seed=5)
+        audio = syn.make_audio(2, 32000, seed=52)
+        mel, logits, feats = run_forward(model, audio)
+        out[name + "__logits_sub4"] = logits[:, ::4].numpy()
+        out[name + "__tokens"] = logits.argmax(-1).numpy().astype(np.int32)
+    for name, seed, B, L, Di, N in STATEDIM_SCANS:
+        x, dt, Bm, Cm, A_log, D = scan_inputs(seed, B, L, Di, N)
+        ssm = SelectiveSSM(d_model=Di // 2, state_dim=N, expand_ratio=2)
+        with torch.no_grad():
+            ssm.D.copy_(torch.from_numpy(D))
+            A = -torch.exp(torch.from_numpy(A_log))
+            tx, tdt, tB, tC = (torch.from_numpy(v) for v in (x, dt, Bm, Cm))
+            out[name + "__parallel"] = ssm._parallel_scan(tx, tdt, A, tB, tC).numpy()
+            out[name + "__sequential"] = ssm._sequential_scan(tx, tdt, A, tB, tC).numpy()
+    out["meta"] = meta(configs=STATEDIM_CFGS, weights_seed=5, audio="make_audio(2, 32000, seed=52)",
+                       scans=[list(c) for c in STATEDIM_SCANS],
+                       scan_inputs="tests/golden/gen_goldens.py:scan_inputs(seed,B,L,Di,N)")
+    save("fwd_statedims.npz", **out)
+
+
 # --------------------------------------------------------------------------- CLI output
 CLI_CLIPS = {"clip_2s.wav": ("make_audio(1, 32000, seed=91)[0]", lambda: syn.make_audio(1, 32000, seed=91)[0]),
              "chirp_3s.wav": ("make_chirp(48000)", lambda: syn.make_chirp(48000)),
@@ -561,7 +593,7 @@ def gen_cli():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["mel", "scan", "forward", "sequential", "small", "decode", "int8", "bf16", "beam",
-                             "fullbatch", "cli"]
+                             "fullbatch", "cli", "statedims"]
     if "mel" in which:
         gen_mel()
     if "scan" in which:
@@ -584,5 +616,7 @@ if __name__ == "__main__":
         gen_fullbatch()
     if "benchsets" in which:  # long (~30 min on 8 threads): not in the default list
         gen_benchsets()
+    if "statedims" in which:
+        gen_statedims()
     if "cli" in which:
         gen_cli()

@@ -463,6 +463,53 @@ def test_small_config(va):
     np.testing.assert_array_equal(logits.argmax(-1).cpu().numpy(), g["tokens"])
 
 
+def _statedims():
+    return golden("fwd_statedims.npz"), json.loads(str(golden("fwd_statedims.npz")["meta"]))
+
+
+@pytest.mark.parametrize("name", ["sd8", "sd48", "sd128"])
+def test_state_dims_model_vs_reference(va, name):
+    """any ssm_state_dim / global_ssm_state_dim (model.py:23-68).  N = 8 and
+    48 run as 16 / 64 with zero-padded states (SelectiveSSM._prepared), N = 128 natively;
+    logits and tokens vs the reference at N = 8, 48, 128 (global 8, 24, 128)."""
+    g, meta = _statedims()
+    m = make_model(va, meta["configs"][name], seed=5)
+    logits = m(va.compute_mel_spectrogram(t(S.make_audio(2, 32000, seed=52)))).cpu().numpy()
+    assert_logits(logits[:, ::4], g[name + "__logits_sub4"])
+    np.testing.assert_array_equal(logits.argmax(-1), g[name + "__tokens"])
+
+
+@pytest.mark.parametrize("case", [tuple(c) for c in json.loads(str(golden("fwd_statedims.npz")["meta"]))["scans"]],
+                         ids=lambda c: c[0])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_scan_state_dims_vs_reference(va, case, mode):
+    """The scan op at N = 8, 48 (zero-padded to 16 / 64 by ops.ssm_scan) and 128 vs the reference."""
+    name, seed, B, L, Di, N = case
+    g, _ = _statedims()
+    x, dt, Bm, Cm, A_log, D = _scan_inputs(seed, B, L, Di, N)
+    got = _run_scan(x, dt, Bm, Cm, A_log, D, mode)
+    want = g[name + ("__sequential" if mode == 1 else "__parallel")]
+    np.testing.assert_allclose(got, want, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("L", [1, 33, 513, 1501])
+def test_scan_n128_chunked_bitwise_and_oracle(va, L):
+    """N = 128 (32 lanes per channel): streaming and chunk-parallel forms bitwise equal, and vs
+    the oracle."""
+    from velocity_asr import ops
+    x, dt, Bm, Cm, A_log, D = _scan_inputs(500 + L, 1, L, 16, 128)
+    prev = ops.scan_form("streaming")
+    try:
+        a = _run_scan(x, dt, Bm, Cm, A_log, D, 2)
+        ops.scan_form("chunked")
+        b = _run_scan(x, dt, Bm, Cm, A_log, D, 2)
+    finally:
+        ops.scan_form(prev)
+    np.testing.assert_array_equal(a, b)
+    ref = R.parallel_scan(x, dt, (-np.exp(A_log)).astype(np.float32), Bm, Cm, D)
+    np.testing.assert_allclose(a, ref, atol=1e-4, rtol=1e-4)
+
+
 # ----------------------------------------------------------------------------- full-size properties
 def _assert_tokens_pinned(got_argmax, got_lists, g, prefix, what):
     """Argmax tokens and greedy lists equal to the reference's, with the frames that differ

@@ -212,3 +212,29 @@ def test_decode_cases():
         assert R.ctc_greedy_decode(lg, collapse_repeated=False) == c["greedy_nocollapse"], name
         ts = R.ctc_greedy_decode_with_timestamps(lg)
         assert [[t, [list(x) for x in s]] for t, s in ts] == c["timestamps"], name
+
+
+def _statedim_meta():
+    return json.loads(str(golden("fwd_statedims.npz")["meta"]))
+
+
+@pytest.mark.parametrize("name", ["sd8", "sd48", "sd128"])
+def test_forward_state_dims(name):
+    """Any ssm_state_dim / global_ssm_state_dim (model.py:23-68): the oracle
+    at N = 8, 48, 128 vs the reference (tests/golden/fwd_statedims.npz)."""
+    g = golden("fwd_statedims.npz")
+    cfg = dict(S.DEFAULT_CONFIG, **_statedim_meta()["configs"][name])
+    W = S.make_weights(cfg, seed=5)
+    logits = R.forward(W, R.compute_mel_spectrogram(S.make_audio(2, 32000, seed=52)), cfg)
+    np.testing.assert_allclose(logits[:, ::4], g[name + "__logits_sub4"], atol=5e-4, rtol=1e-4)
+    np.testing.assert_array_equal(logits.argmax(-1), g[name + "__tokens"])
+
+
+@pytest.mark.parametrize("case", [tuple(c) for c in _statedim_meta()["scans"]], ids=lambda c: c[0])
+def test_scan_state_dims(case):
+    name, seed, B, L, Di, N = case
+    g = golden("fwd_statedims.npz")
+    x, dt, Bm, Cm, A_log, D = scan_inputs(seed, B, L, Di, N)
+    A = (-np.exp(A_log)).astype(np.float32)
+    np.testing.assert_allclose(R.parallel_scan(x, dt, A, Bm, Cm, D), g[name + "__parallel"], atol=5e-5, rtol=5e-5)
+    np.testing.assert_allclose(R.sequential_scan(x, dt, A, Bm, Cm, D), g[name + "__sequential"], atol=5e-5, rtol=5e-5)

@@ -1,0 +1,239 @@
+// Selective-SSM scan + D skip + SiLU gate (reference velocity_asr/ssm.py:119-129): the kernels.
+// Included by scan_n{16,32,64,128}.hip, one translation unit per state dim (they compile in
+// parallel); scan.hip holds the C ABI entry points.
+//
+// mode 0 reproduces the reference's DEFAULT scan_mode="parallel": _associative_scan
+// (ssm.py:216-295), a Blelloch up/down sweep over the time axis padded to a power of two
+// whose down-sweep combine re-uses the already-updated right operand and whose result is
+// the EXCLUSIVE prefix.  Instead of materialising (B, P, Di, N) arrays
+// the kernel streams time and keeps, per state lane, a binary-counter stack of aligned
+// blocks: (la, lb) = the block's up-sweep composite, (ca, cb) = the down-sweep prefix right
+// after the block.  Pushing element t merges it with its left siblings exactly as the
+// up-sweep does and derives (ca, cb) exactly as the down-sweep does, so every float
+// operation of the reference tree is performed once, in the same order (the numpy oracle's
+// associative_scan_stream is bitwise equal to the literal tree; see oracle/velocity_ref.py).
+// The only deviation from the reference arithmetic is exp: dA = exp2(dt * A*log2e) on the
+// hardware v_exp_f32 (a few ULP) instead of torch's CPU exp.  Contraction is disabled so
+// a*b + c stays two roundings as in the reference.
+//
+// mode 1 is the true recurrence of scan_mode="sequential" (ssm.py:134-171).
+//
+// Work decomposition (MI355X): one workgroup = (utterance b, DPB consecutive channels d),
+// 4 waves.  G = N/4 lanes share one channel and each lane owns 4 state indices n, held as
+// two float2 pairs so the state algebra issues as packed v_pk_mul/v_pk_add_f32 (two lanes'
+// worth of fp32 per instruction: the f32 vector peak); tiny launches use G = N/2 lanes with
+// 2 state indices each (scan_body.inc is compiled for both layouts).  Per time step each lane leaves its
+// partial y = sum_n h C in an LDS tile; the chunk's gated outputs are reduced and written
+// from LDS as coalesced row segments.  Time runs in 16-step chunks: x, dt, z, B, C slices
+// are staged to LDS (double-buffered, register prefetch of the next chunk); the four
+// in-chunk stack levels are compile-time registers (step i's push/merge pattern is a
+// constant, full chunks carry no per-step guards); chunk-sized blocks form the upper stack,
+// merged once per chunk.  Launches of at most two waves per SIMD run 32-step chunks (five
+// in-chunk levels; see launch_n).  Blocks are remapped so all channel blocks of one utterance share
+// an XCD (its 4 MiB L2 then serves the B/C slices and the 64-B row segments they share).
+#pragma once
+
+#include "vasr_internal.h"
+
+namespace vasr {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+#ifndef VASR_SCAN_ABLATE
+#define VASR_SCAN_ABLATE 0  // diagnostic builds only (tools/scan_ablate.sh): 1 no exp,
+#endif                      // 4 no B/C LDS reads, 8 no chunk staging after the first,
+                            // 16 no tree update, 32 no gated-output pass
+#ifndef VASR_SCAN_WAVES
+#define VASR_SCAN_WAVES 3   // waves per SIMD the register allocator targets
+#endif
+#ifndef VASR_SCAN_WAVES_NPL2
+#define VASR_SCAN_WAVES_NPL2 4  // the same for the 2-states-per-lane layout
+#endif
+#ifndef VASR_SCAN_WAVES_TC32
+#define VASR_SCAN_WAVES_TC32 2  // the 32-step-chunk kernel (VASR_SCAN_T=32): one more stack level
+#endif
+#ifndef VASR_SCAN_FASTSTAGE
+#define VASR_SCAN_FASTSTAGE 1  // 0: every chunk's staging addresses from the clamped index path
+#endif
+#ifndef VASR_SCAN_PACKED
+#define VASR_SCAN_PACKED 1  // 1: state pairs as float2 vectors (v_pk_*_f32); 0: scalar pairs
+#endif
+
+// A pair of state values.  Packed v_pk_mul/add_f32 issue at half the rate of their scalar
+// forms on gfx950 (no FLOP gain) but halve the instruction count; measured 4 % faster than
+// scalar pairs here (tools/scan_ablate.sh), so packed is the default.
+#if VASR_SCAN_PACKED
+typedef float f2 __attribute__((ext_vector_type(2)));
+#else
+struct f2 {
+    float x, y;
+};
+__device__ __forceinline__ f2 operator*(f2 a, f2 b) { return f2{a.x * b.x, a.y * b.y}; }
+__device__ __forceinline__ f2 operator+(f2 a, f2 b) { return f2{a.x + b.x, a.y + b.y}; }
+#endif
+
+constexpr float LOG2E_F = 1.4426950408889634f;
+constexpr int T = 16;    // time steps per chunk (the chunk-parallel form; the streaming kernel's TC)
+constexpr int TP = T + 1;  // padded row of the per-channel partial-sum tile
+constexpr int NW = 4;    // waves per block
+
+constexpr int ctz_c(int v) { return v & 1 ? 0 : 1 + ctz_c(v >> 1); }
+constexpr int trailing_ones(int v) { return v & 1 ? 1 + trailing_ones(v >> 1) : 0; }
+// Level of the stack entry right below a new block at level j after step i (count i+1),
+// or -1 when the entry below is the upper (chunk-level) stack.
+// lg = in-chunk stack levels (log2 of the chunk length).
+constexpr int below_level(int i, int j, int lg = 4) {
+    return ((i + 1) >> (j + 1)) == 0 ? -1
+           : (j + 1 + ctz_c((i + 1) >> (j + 1)) < lg ? j + 1 + ctz_c((i + 1) >> (j + 1)) : -1);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+// lane ^ 16 within each 32-lane half (ds_swizzle bit mode: and 0x1F, or 0, xor 0x10); DPP
+// cannot cross a 16-lane row
+__device__ __forceinline__ float swz_xor16(float x) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x401F));
+}
+
+// Sum over aligned groups of G lanes (G in {4, 8, 16, 32}); every lane gets the sum.
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+    v += dpp_mov<0xB1>(v);                          // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);                          // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += dpp_mov<0x141>(v);   // row_half_mirror
+    if constexpr (G >= 16) v += dpp_mov<0x140>(v);  // row_mirror
+    if constexpr (G >= 32) v += swz_xor16(v);
+    return v;
+}
+
+// partner exchange of a butterfly level: a DPP control, or -1 for lane ^ 16
+template <int CTRL>
+__device__ __forceinline__ float xchg(float x) {
+    if constexpr (CTRL < 0) return swz_xor16(x);
+    else return dpp_mov<CTRL>(x);
+}
+
+constexpr int log2_c(int v) { return v <= 1 ? 0 : 1 + log2_c(v >> 1); }
+
+// Cross-lane reduction of 8 per-step partial sums over the G lanes of a channel, as a
+// transposing butterfly: each level halves the values a lane holds by exchanging the half it
+// gives away with its partner (DPP), so the 8 sums cost 7 exchanges and no wait states
+// (independent chains) instead of 8 dependent group_sum chains.  Partner masks xor 15, 7,
+// 2, 1 (row_mirror, row_half_mirror, quad_perm) keep partners in the same step subset.
+// Returns in v[0 .. S_f) the sums of steps j + S_f * (g >> (log2 G - nsplit)).
+template <int G>
+struct HalfReduce {
+    static constexpr int LG = log2_c(G);
+    static constexpr int NSPLIT = LG < 3 ? LG : 3;
+    static constexpr int SF = 8 >> NSPLIT;
+    static __device__ __forceinline__ int step(int j, int g) { return j + SF * (g >> (LG - NSPLIT)); }
+};
+
+template <int CTRL, int S>
+__device__ __forceinline__ void butterfly_level(float (&v)[8], bool sel) {
+    if constexpr (S >= 2) {
+#pragma unroll
+        for (int j = 0; j < S / 2; ++j) {
+            const float lo = v[j], hi = v[j + S / 2];
+            const float keep = sel ? hi : lo;
+            const float send = sel ? lo : hi;
+            v[j] = keep + xchg<CTRL>(send);
+        }
+    } else {
+        v[0] = v[0] + xchg<CTRL>(v[0]);
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void reduce_half(float (&v)[8], int g) {
+    if constexpr (G == 32) {
+        butterfly_level<-1, 8>(v, (g >> 4) & 1);     // ds_swizzle: lane ^ 16
+        butterfly_level<0x140, 4>(v, (g >> 3) & 1);  // row_mirror: lane ^ 15
+        butterfly_level<0x141, 2>(v, (g >> 2) & 1);  // row_half_mirror: lane ^ 7
+        butterfly_level<0x4E, 1>(v, false);          // quad_perm [2,3,0,1]: lane ^ 2
+        butterfly_level<0xB1, 1>(v, false);          // quad_perm [1,0,3,2]: lane ^ 1
+    } else if constexpr (G == 16) {
+        butterfly_level<0x140, 8>(v, (g >> 3) & 1);  // row_mirror: lane ^ 15
+        butterfly_level<0x141, 4>(v, (g >> 2) & 1);  // row_half_mirror: lane ^ 7
+        butterfly_level<0x4E, 2>(v, (g >> 1) & 1);   // quad_perm [2,3,0,1]: lane ^ 2
+        butterfly_level<0xB1, 1>(v, false);          // quad_perm [1,0,3,2]: lane ^ 1
+    } else if constexpr (G == 8) {
+        butterfly_level<0x141, 8>(v, (g >> 2) & 1);
+        butterfly_level<0x4E, 4>(v, (g >> 1) & 1);
+        butterfly_level<0xB1, 2>(v, g & 1);
+    } else {
+        static_assert(G == 4, "G in {4, 8, 16, 32}");
+        butterfly_level<0x4E, 8>(v, (g >> 1) & 1);
+        butterfly_level<0xB1, 4>(v, g & 1);
+    }
+}
+
+// Reduce the partial sums of steps [8*HALF, 8*HALF + 8) and store them to the channel's row
+// of the partial-sum tile ([DPB][TC + 1] floats; TC = chunk length).
+template <int G, int HALF, int TC = T>
+__device__ __forceinline__ void flush_half(float (&yv)[TC], float* yp, int dl, int g) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = yv[HALF * 8 + j];
+    reduce_half<G>(v, g);
+#pragma unroll
+    for (int j = 0; j < HalfReduce<G>::SF; ++j) yp[dl * (TC + 1) + HALF * 8 + HalfReduce<G>::step(j, g)] = v[j];
+}
+
+// a * b + c: two roundings as in the reference tree (modes 0), or one fused multiply-add
+// (mode 2: v_pk_fma_f32, a third fewer state-update instructions)
+template <bool FMA>
+__device__ __forceinline__ f2 mad2(f2 a, f2 b, f2 c) {
+#pragma clang fp contract(off)
+    if constexpr (FMA) {
+#if VASR_SCAN_PACKED
+        return __builtin_elementwise_fma(a, b, c);
+#else
+        return f2{__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y)};
+#endif
+    } else {
+        return a * b + c;
+    }
+}
+
+__device__ __forceinline__ f2 exp2v(f2 v) {
+    f2 r;
+    r.x = __builtin_amdgcn_exp2f(v.x);
+    r.y = __builtin_amdgcn_exp2f(v.y);
+    return r;
+}
+
+// The kernel body for each lane layout (scan_body.inc): npl4 = 4 state indices per lane
+// (G = N/4 lanes per channel), npl2 = 2 per lane (twice the waves for the same work).
+// (npl2 first: the chunk-parallel launcher of either layout uses npl2's block-level kernel)
+namespace npl2 {
+constexpr int NPL = 2;
+#include "scan_body.inc"
+}  // namespace npl2
+namespace npl4 {
+constexpr int NPL = 4;
+#include "scan_body.inc"
+}  // namespace npl4
+
+}  // namespace
+}  // namespace vasr
+
+namespace vasr {
+// Per-state-dim launchers (scan_n<N>.hip): two = 2 state indices per lane (npl2), else 4.
+#define VASR_SCAN_LAUNCHERS(NN)                                                                                    \
+    int scan_streaming_n##NN(bool two, int mode, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,   \
+                             const float* bc, int64_t ld_bc, const float* A2, const float* D, float* out,           \
+                             int64_t ld_out, int B, int L, int Di, hipStream_t s);                                  \
+    int scan_chunked_n##NN(bool two, int mode, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,     \
+                           const float* bc, int64_t ld_bc, const float* A2, const float* D, float* out,             \
+                           int64_t ld_out, int B, int L, int Di, float* ws_a, float* ws_b, hipStream_t s);
+VASR_SCAN_LAUNCHERS(16)
+VASR_SCAN_LAUNCHERS(32)
+VASR_SCAN_LAUNCHERS(64)
+VASR_SCAN_LAUNCHERS(128)
+#undef VASR_SCAN_LAUNCHERS
+}  // namespace vasr

@@ -425,10 +425,31 @@ def _use_chunked(B: int, Lq: int, Di: int, N: int, mode: int) -> bool:
     return B * Di * N // 256 < CHUNKED_MAX_WAVES
 
 
+SCAN_STATE_DIMS = (16, 32, 64, 128)  # the scan kernels' state dims (include/vasr.h)
+
+
+def scan_state_dim(N: int) -> int:
+    """The kernel state dim a state dim N runs as: N itself, or the next size up with the
+    padded states zero (they stay 0 and add nothing to y)."""
+    for n in SCAN_STATE_DIMS:
+        if N <= n:
+            return n
+    raise NotImplementedError(f"selective scan: state dim {N} > {SCAN_STATE_DIMS[-1]} not supported")
+
+
 def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Tensor, D: torch.Tensor, B: int,
              Lq: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Gated selective scan.  xz (B*L, 2Di) [x|z], dt (B*L, Di), bc (B*L, 2N) [B|C] (row views).
-    Small launches of the tree modes take the chunk-parallel form (same results, bitwise)."""
+    Small launches of the tree modes take the chunk-parallel form (same results, bitwise).
+    A state dim without a kernel instance (scan_state_dim) is zero-padded here, a copy of bc
+    (the model avoids it: its projection GEMM writes the padded layout, SelectiveSSM._prepared)."""
+    N0 = A2.numel()
+    Np = scan_state_dim(N0)
+    if Np != N0:
+        Bm, Cm = bc[:, :N0], bc[:, N0:2 * N0]
+        pad = torch.zeros((bc.shape[0], Np - N0), device=bc.device, dtype=bc.dtype)
+        bc = torch.cat([Bm, pad, Cm, pad], 1)
+        A2 = torch.cat([A2, torch.zeros(Np - N0, device=A2.device, dtype=A2.dtype)])
     D = f32(D)
     for n, t in (("xz", xz), ("dt", dt), ("bc", bc), ("A2", A2), ("D", D)):
         _cuda_f32(f"ssm_scan.{n}", t)

@@ -76,13 +76,22 @@ class SelectiveSSM(nn.Module):
     def _prepared(self):
         def build():
             dev = self.x_proj.weight.device
-            w = torch.cat([self.x_proj.weight, self.dt_proj.weight], 0).contiguous()
-            b = torch.cat([torch.zeros(2 * self.state_dim, device=dev), self.dt_proj.bias.float()]).contiguous()
+            N, Np = self.state_dim, ops.scan_state_dim(self.state_dim)
+            xw = self.x_proj.weight
+            if Np != N:
+                # state dims the scan kernels are not built for run as the next size up: zero rows
+                # make the GEMM write B and C with Np - N zero columns each, and A2 = 0 there, so
+                # the padded states stay exactly 0 and add nothing to y (include/vasr.h)
+                z = torch.zeros(Np - N, xw.shape[1], device=dev, dtype=xw.dtype)
+                xw = torch.cat([xw[:N], z, xw[N:], z], 0)
+            w = torch.cat([xw, self.dt_proj.weight], 0).contiguous()
+            b = torch.cat([torch.zeros(2 * Np, device=dev), self.dt_proj.bias.float()]).contiguous()
             # A = -exp(A_log) exactly as the reference evaluates it (float32, ssm.py:116), then
             # pre-scaled by log2(e) so the kernel's dA is one v_exp_f32.
             A = -torch.exp(self.A_log.detach().float().cpu())
-            A2 = (A * torch.tensor(ops.LOG2E, dtype=torch.float32)).to(dev)
-            out = dict(w_xdt=w, b_xdt=b, A2=A2)
+            A2 = torch.zeros(Np, dtype=torch.float32)
+            A2[:N] = A * torch.tensor(ops.LOG2E, dtype=torch.float32)
+            out = dict(w_xdt=w, b_xdt=b, A2=A2.to(dev))
             if w.dtype == torch.float32:
                 # composed projection: [x_proj; dt_proj](in_proj_x(u)) = u @ (W_xdt W_in_x)^T, the
                 # product formed in float64 and rounded once (see gated_scan)
@@ -111,7 +120,7 @@ class SelectiveSSM(nn.Module):
         launch instead of two and no re-read of x_p.  VASR_XDT_COMPOSE=0 selects the two
         products as the reference evaluates them (ssm.py:105-113)."""
         p = self._prepared()
-        Di, N = self.d_inner, self.state_dim
+        Di, N = self.d_inner, ops.scan_state_dim(self.state_dim)
         if "w_comb" in p and os.environ.get("VASR_XDT_COMPOSE", "1") != "0":
             out = ops.gemm(u, p["w_comb"], p["b_comb"], epilogue=_lib.EPI_SOFTPLUS_FROM,
                            n_out=2 * Di + 2 * N)                                 # (M, 2Di + 2N + Di)
@@ -124,7 +133,7 @@ class SelectiveSSM(nn.Module):
     def scan(self, xz: torch.Tensor, xdt: torch.Tensor, B: int, L: int) -> torch.Tensor:
         """The gated scan over in_proj's [x | z] and [B | C | dt]."""
         p = self._prepared()
-        N = self.state_dim
+        N = ops.scan_state_dim(self.state_dim)
         mode = _SCAN_MODE_ID[self.scan_mode]
         return ops.ssm_scan(xz, xdt[:, 2 * N:], xdt[:, :2 * N], p["A2"], self.D, B, L,
                             _tree_mode() if mode == 0 else mode)
