@@ -112,6 +112,35 @@ def test_flac_crc_and_format_errors(tmp_path):
         _decode_bytes(tmp_path, bytes(data[:60]))
 
 
+def _stream(frames, bps, n, sr=16000):
+    """fLaC + a lone STREAMINFO block (bps, n samples) + the given frames."""
+    info = FW.streaminfo(sr, 1, bps, n)
+    return b"fLaC" + bytes([0x80]) + len(info).to_bytes(3, "big") + info + b"".join(frames)
+
+
+def test_flac_rejects_corrupt_streams(tmp_path):
+    """Frames whose sample size differs from STREAMINFO, and predictors whose decoded samples
+    leave the sample size (a corrupt residual), end the decode with an error."""
+    x = _sig(1024, 16, 6)[0]
+    ok = _stream([FW.frame(0, [x], 16, 16000)], 16, 1024)
+    wav, _ = _decode_bytes(tmp_path, ok)
+    np.testing.assert_array_equal(wav.numpy()[0], _expect([x], 16)[0])
+    with pytest.raises(ValueError, match="sample size differs"):
+        _decode_bytes(tmp_path, _stream([FW.frame(0, [x], 24, 16000)], 16, 1024))
+    ramp = 30000 + 500 * np.arange(64, dtype=np.int64)  # leaves int16 after 6 samples
+    for kind in ("fixed", "lpc"):
+        bad = _stream([FW.frame(0, [ramp], 16, 16000, sub=[dict(kind=kind, order=2)])], 16, 64)
+        with pytest.raises(ValueError, match="exceeds the sample size"):
+            _decode_bytes(tmp_path, bad)
+
+
+def test_resample_rejects_huge_kernels():
+    """Coprime rates (44101 -> 16000 Hz) would need a 16000 x 44135-tap kernel: refused."""
+    from velocity_asr.audio import resample
+    with pytest.raises(Exception, match="tap kernel"):
+        resample(torch.zeros(100), 44101, 16000)
+
+
 def _resample_ref(x, orig, new):
     """float64 numpy restatement of torchaudio.functional.resample (sinc_interp_hann,
     lowpass_filter_width 6, rolloff 0.99): kernel in float64 rounded to float32, stride-orig

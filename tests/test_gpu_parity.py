@@ -553,3 +553,26 @@ def test_full_batch_30s_pinned(va, model):
     g = golden("fwd_fullbatch.npz")
     _assert_tokens_pinned(logits.argmax(-1).cpu().numpy(), va.ctc_greedy_decode(logits), g, "c4_",
                           "C4 8 x 30 s")
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 64, 192), (33, 1280, 192), (501, 1280, 192), (8016, 1280, 192),
+                                   (300, 1000, 192), (129, 96, 128), (77, 200, 100), (1024, 192, 192)])
+@pytest.mark.parametrize("epi", ["none", "gelu", "softplus", "residual", "argmax"])
+def test_gemm_rows_engine_bitwise_equals_tiles(va, M, N, K, epi):
+    """The A-rows-stationary split GEMM (gemm_rows.hip, K = 128 / 192 after padding to 32)
+    performs the tile kernel's MFMA sequence per output element: bitwise equal outputs, for
+    every unpaired epilogue, ragged M and N, and K below the padded width."""
+    from velocity_asr import _lib, ops
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    a = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    kw = {"none": dict(epilogue=_lib.EPI_NONE), "gelu": dict(epilogue=_lib.EPI_GELU),
+          "softplus": dict(epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=N // 3),
+          "residual": dict(epilogue=_lib.EPI_RESIDUAL, aux=res)}.get(epi)
+    out = {}
+    for eng in (1, 2):
+        with ops.option(_lib.OPT_GEMM_ENGINE, eng):
+            out[eng] = ops.gemm_argmax(a, w, b) if epi == "argmax" else ops.gemm(a, w, b, **kw)
+    assert torch.equal(out[1], out[2])

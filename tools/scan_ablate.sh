@@ -10,7 +10,8 @@ i=0
 for v in $VARIANTS; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include ${flags//,/ } \
-     -fno-slp-vectorize -ffp-contract=off -shared csrc/scan.hip csrc/common.cpp -o $OUT/lib_${i}_${name}.so &
+     -fno-slp-vectorize -ffp-contract=off -shared csrc/scan.hip csrc/scan_n16.hip csrc/scan_n32.hip csrc/scan_n64.hip \
+     csrc/scan_n128.hip csrc/common.cpp -o $OUT/lib_${i}_${name}.so &
   i=$((i+1))
 done
 wait

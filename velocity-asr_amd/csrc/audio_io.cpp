@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <vector>
 
 #include "vasr_internal.h"
@@ -181,6 +182,11 @@ bool read_residual(BitReader& br, int bs, int order, int32_t* res, const char*& 
     return true;
 }
 
+// A decoded sample must fit the subframe's sample size; a corrupt residual that does not would
+// feed ever-growing values into the predictors (and, at 32 taps of 15-bit coefficients, overflow
+// their int64 sums), so it ends the decode instead.
+inline bool fits(int64_t v, int bps) { return v >= -((int64_t)1 << (bps - 1)) && v < ((int64_t)1 << (bps - 1)); }
+
 bool read_subframe(BitReader& br, int bs, int bps, int64_t* out, std::vector<int32_t>& res, const char*& err) {
     if (br.bit() != 0) {
         err = "subframe padding bit set";
@@ -218,6 +224,10 @@ bool read_subframe(BitReader& br, int bs, int bps, int64_t* out, std::vector<int
                 default: break;
             }
             out[i] = pred + res[i];
+            if (!fits(out[i], bps)) {
+                err = "fixed-predictor sample exceeds the sample size";
+                return false;
+            }
         }
     } else if (type >= 32) {  // LPC
         const int order = type - 31;
@@ -244,6 +254,10 @@ bool read_subframe(BitReader& br, int bs, int bps, int64_t* out, std::vector<int
             int64_t acc = 0;
             for (int j = 0; j < order; ++j) acc += coef[j] * out[i - 1 - j];
             out[i] = (acc >> shift) + res[i];
+            if (!fits(out[i], bps)) {
+                err = "LPC sample exceeds the sample size";
+                return false;
+            }
         }
     } else {
         err = "reserved subframe type";
@@ -257,6 +271,9 @@ bool read_subframe(BitReader& br, int bs, int bps, int64_t* out, std::vector<int
         for (int i = 0; i < bs; ++i) out[i] = (int64_t)((uint64_t)out[i] << wasted);
     return true;
 }
+
+// Per-channel cap on decoded samples (2^28: 4.6 h at 16 kHz, 2 GiB of int64 per channel).
+constexpr int64_t kMaxFlacSamples = (int64_t)1 << 28;
 
 // Decode every frame; samples[c] grows per channel.
 bool decode_frames(const uint8_t* d, int64_t n, const StreamInfo& si, std::vector<std::vector<int64_t>>& samples,
@@ -318,12 +335,15 @@ bool decode_frames(const uint8_t* d, int64_t n, const StreamInfo& si, std::vecto
             return false;
         }
         (void)kRates;
-        int bps = sz_code == 0 ? si.bps : kBits[sz_code];
+        const int bps = sz_code == 0 ? si.bps : kBits[sz_code];
         if (bps <= 0) {
             err = "reserved sample size code";
             return false;
         }
-        bps_out = bps;
+        if (bps != si.bps) {  // one scale for the whole stream (vasr_flac_decode divides by 2^(bps-1))
+            err = "frame sample size differs from STREAMINFO";
+            return false;
+        }
         const int64_t hdr_bytes = br.pos / 8;
         const uint8_t hcrc = (uint8_t)br.bits(8);
         if (br.overrun || crc8(d + off, hdr_bytes) != hcrc) {
@@ -365,6 +385,10 @@ bool decode_frames(const uint8_t* d, int64_t n, const StreamInfo& si, std::vecto
                 sub[1][i] = (mid - side) >> 1;
             }
         }
+        if ((int64_t)samples[0].size() + bs > kMaxFlacSamples) {
+            err = "stream exceeds the decoder's sample limit";
+            return false;
+        }
         for (int c = 0; c < nch; ++c) samples[c].insert(samples[c].end(), sub[c].begin(), sub[c].begin() + bs);
         off += body + 2;
     }
@@ -376,8 +400,9 @@ bool decode_frames(const uint8_t* d, int64_t n, const StreamInfo& si, std::vecto
 }  // namespace
 }  // namespace vasr
 
-VASR_API int vasr_flac_decode(const uint8_t* data, int64_t n, float* out, int64_t out_cap, int* channels,
-                              int* sample_rate, int* bits, int64_t* samples) {
+namespace {
+int flac_decode(const uint8_t* data, int64_t n, float* out, int64_t out_cap, int* channels, int* sample_rate, int* bits,
+                int64_t* samples) {
     using namespace vasr;
     VASR_CHECK_ARG(data && n > 0 && channels && sample_rate && bits && samples, "vasr_flac_decode: null argument");
     StreamInfo si;
@@ -388,6 +413,10 @@ VASR_API int vasr_flac_decode(const uint8_t* data, int64_t n, float* out, int64_
     }
     std::vector<std::vector<int64_t>> pcm;
     int bps = si.bps;
+    if (bps < 4 || bps > 32) {
+        set_error("vasr_flac_decode: STREAMINFO sample size %d outside 4..32", bps);
+        return VASR_EINVAL;
+    }
     if (!decode_frames(data, n, si, pcm, bps, err)) {
         set_error("vasr_flac_decode: %s", err);
         return VASR_EINVAL;
@@ -404,6 +433,18 @@ VASR_API int vasr_flac_decode(const uint8_t* data, int64_t n, float* out, int64_
     for (int c = 0; c < si.channels; ++c)
         for (int64_t i = 0; i < ns; ++i) out[c * ns + i] = (float)((double)pcm[c][i] * scale);
     return VASR_OK;
+}
+}  // namespace
+
+// The host entry points allocate (decoded PCM, resampling kernels): no exception crosses the C ABI.
+VASR_API int vasr_flac_decode(const uint8_t* data, int64_t n, float* out, int64_t out_cap, int* channels,
+                              int* sample_rate, int* bits, int64_t* samples) {
+    try {
+        return flac_decode(data, n, out, out_cap, channels, sample_rate, bits, samples);
+    } catch (const std::exception& e) {
+        vasr::set_error("vasr_flac_decode: %s", e.what());
+        return VASR_EINVAL;
+    }
 }
 
 // torchaudio.functional.resample with Resample()'s defaults (sinc_interp_hann, lowpass filter
@@ -423,8 +464,8 @@ VASR_API int64_t vasr_resample_length(int64_t n, int orig_sr, int new_sr) {
     return (w * n + o - 1) / o;
 }
 
-VASR_API int vasr_resample_f32(const float* x, int channels, int64_t n, int64_t ld_x, int orig_sr, int new_sr, float* y,
-                               int64_t ld_y) {
+namespace {
+int resample_f32(const float* x, int channels, int64_t n, int64_t ld_x, int orig_sr, int new_sr, float* y, int64_t ld_y) {
     using namespace vasr;
     VASR_CHECK_ARG(x && y && channels > 0 && n > 0 && orig_sr > 0 && new_sr > 0 && ld_x >= n,
                    "vasr_resample_f32: bad arguments");
@@ -445,6 +486,11 @@ VASR_API int vasr_resample_f32(const float* x, int channels, int64_t n, int64_t 
     const double base = (double)(orig < nw ? orig : nw) * rolloff;
     const int width = (int)std::ceil(lpw * orig / base);
     const int klen = 2 * width + orig;
+    // (new, 2 * width + orig) taps after the gcd reduction: rates with a small gcd (44101 -> 16000)
+    // would need gigabytes of kernel
+    VASR_CHECK_ARG((int64_t)nw * klen <= ((int64_t)1 << 24),
+                   "vasr_resample_f32: %d -> %d Hz needs a %lld-tap kernel (limit 2^24)", orig_sr, new_sr,
+                   (long long)nw * klen);
     std::vector<float> kern((size_t)nw * klen);
     const double pi = 3.14159265358979323846;
     for (int j = 0; j < nw; ++j) {
@@ -475,4 +521,15 @@ VASR_API int vasr_resample_f32(const float* x, int channels, int64_t n, int64_t 
         }
     }
     return VASR_OK;
+}
+}  // namespace
+
+VASR_API int vasr_resample_f32(const float* x, int channels, int64_t n, int64_t ld_x, int orig_sr, int new_sr, float* y,
+                               int64_t ld_y) {
+    try {
+        return resample_f32(x, channels, n, ld_x, orig_sr, new_sr, y, ld_y);
+    } catch (const std::exception& e) {
+        vasr::set_error("vasr_resample_f32: %s", e.what());
+        return VASR_EINVAL;
+    }
 }

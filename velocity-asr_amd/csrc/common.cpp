@@ -28,9 +28,9 @@ VASR_API const char* vasr_last_error(void) { return vasr::g_last_error; }
 
 // Tuning options (vasr_set_option): process-wide, defaults from the environment read once.
 namespace {
-constexpr int kNumOptions = 3;
-const char* const kOptionEnv[kNumOptions] = {"VASR_SCAN_NPL", "VASR_SCAN_T", "VASR_TAIL_ROWS"};
-const int kOptionValues[kNumOptions][3] = {{0, 2, 4}, {0, 16, 32}, {0, 16, 32}};
+constexpr int kNumOptions = 4;
+const char* const kOptionEnv[kNumOptions] = {"VASR_SCAN_NPL", "VASR_SCAN_T", "VASR_TAIL_ROWS", "VASR_GEMM_ENGINE"};
+const int kOptionValues[kNumOptions][3] = {{0, 2, 4}, {0, 16, 32}, {0, 16, 32}, {0, 1, 2}};
 std::atomic<int> g_options[kNumOptions];
 std::once_flag g_options_once;
 

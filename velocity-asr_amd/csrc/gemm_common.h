@@ -317,4 +317,10 @@ inline int check_args(const vasr_gemm_args* a, const char* fn, GemmParams& p) {
 }
 
 }  // namespace gemm
+
+// gemm_rows.hip: launches the A-rows-stationary split GEMM when the shape suits it (batch 1,
+// K = 128 / 192, unpaired epilogue) and the engine option allows; returns true with the launch
+// status in *rc, false when the tile kernel should run.
+bool try_rows_x3(const gemm::GemmParams& p, int batch, int epi, hipStream_t s, int* rc);
+
 }  // namespace vasr

@@ -1,0 +1,340 @@
+// Split-bf16 fp32 GEMM for short K (K <= 16 * KS: the model's K = 192 projections), "A rows
+// stationary": each wave loads its 32 rows of A once, splits them into the three bf16 planes
+// (x = hi + mid + lo, gemm_split.h) and keeps all of them in VGPRs (12 k-steps x 3 planes x
+// bf16x8 = 144 VGPRs at K = 192) for the whole kernel, then walks a run of 32-column W chunks:
+// per chunk 12 k-steps x the same six v_mfma_f32_32x32x16_bf16 products in the same order as
+// the LDS-ring tile kernel (gemm_x3.hip), so the results are bitwise those of that kernel.
+//
+// Why: at K = 192 the tile kernel spends a whole 128 x 128 tile's life in one short K loop and
+// then stores 64 KB of C at the end, in phase with every other block (measured: MFMA phase
+// 12.3 us and store phase 10.8 us per two tiles per CU, serialised).  Here a
+// block owns 256 rows x a run of 32-column chunks, with two accumulator sets: chunk j's MFMAs
+// issue while chunk j-1's epilogue stores (non-temporal) drain, and the W chunks (36 KiB each,
+// in the fragment-native layout of vasr_split_weights_bf16x3, contiguous per chunk) stream
+// through a three-slot LDS ring by LDS-DMA two chunks ahead (issued by four of the eight waves).
+//
+// Work decomposition: block = 8 waves (two per SIMD) x 32 rows = 256 rows, grid = row blocks x
+// column groups (runs of chunks), at most one block per CU so the grid is one round; blocks id,
+// id + 8, ... share an XCD and get consecutive (row block, column group) items, so the column
+// groups of one row block read its A rows from one L2.  Epilogues: gemm_common.h's (unpaired
+// ones), per 32 x 32 chunk.  Measured variants (profiles/r03k): 4 waves per block, cached
+// stores, and store groups of 2-4 chunks (VASR_ROWS_SUPER) were all slower or equal.
+#include <type_traits>
+
+#include "gemm_common.h"
+#include "gemm_split.h"
+
+namespace vasr {
+namespace {
+
+using namespace gemm;
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+// LDS-DMA of 16 B per lane into dst_base + 16 * lane (untracked by the compiler's waitcnt
+// model, ordered by the kernel: counted vmcnt + barrier; the memory clobber keeps the
+// epilogue's stores ahead of it in issue order)
+__device__ __forceinline__ void glds16(const void* src, void* dst_base) {
+    const unsigned lds = (unsigned)(uintptr_t)(lds_void*)dst_base;
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+#ifndef VASR_ROWS_ABLATE
+#define VASR_ROWS_ABLATE 0  // diagnostic builds only: 1 no MFMA, 2 no epilogue stores, 4 no LDS-DMA
+#endif                      // after the first two chunks, 8 no per-chunk barrier
+#ifndef VASR_ROWS_WAVES
+#define VASR_ROWS_WAVES 8  // 256 A rows per block (r03k: 8 waves 37.8 us vs 4 waves 45.0 on the head GEMM)
+#endif
+#ifndef VASR_ROWS_DEPTH
+#define VASR_ROWS_DEPTH 2  // W chunks in flight ahead of the one being multiplied (LDS slots = depth + 1)
+#endif
+#ifndef VASR_ROWS_STORE_AUX
+#define VASR_ROWS_STORE_AUX 2  // cache-policy bits of the epilogue's buffer stores (2 = nt: C is not re-read from L2)
+#endif
+constexpr int RW = VASR_ROWS_WAVES;  // waves per block (4: one per SIMD)
+constexpr int DEPTH = VASR_ROWS_DEPTH;
+constexpr int NSLOT = DEPTH + 1;
+#ifndef VASR_ROWS_SUPER
+#define VASR_ROWS_SUPER 1  // chunks per store group (their epilogues run back to back)
+#endif
+constexpr int SUPER = VASR_ROWS_SUPER;
+static_assert(SUPER >= 1 && SUPER <= 4, "store group of 1..4 chunks");
+constexpr int MAX_GROUP = 40;   // chunks per column group (LDS epilogue tables: 40 x 32 columns)
+
+// s_waitcnt vmcnt(n) for a runtime n in [0, 63] (the immediate has to be a constant)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+    switch (n) {
+#define VASR_W(I) case I: wait_vmcnt<I>(); break;
+#define VASR_W8(B) VASR_W(B) VASR_W(B + 1) VASR_W(B + 2) VASR_W(B + 3) VASR_W(B + 4) VASR_W(B + 5) VASR_W(B + 6) VASR_W(B + 7)
+        VASR_W8(0) VASR_W8(8) VASR_W8(16) VASR_W8(24) VASR_W8(32) VASR_W8(40) VASR_W8(48) VASR_W8(56)
+#undef VASR_W8
+#undef VASR_W
+        default: wait_vmcnt<0>();
+    }
+}
+
+// Epilogue of one 32 x 32 chunk held as one MFMA accumulator (the tile kernel's epilogue_body
+// arithmetic for TM = TN = 1), with the per-column bias / fake-quant parameters read from LDS
+// and the results written by raw buffer stores: exactly NST store instructions per wave and
+// chunk whatever the bounds (out-of-range lanes get an offset past the buffer's num_records,
+// which the hardware drops), so the kernel's counted vmcnt waits stay exact.  No vector-memory
+// loads besides the residual / positional operand, so the compiler's own vmcnt waits for those
+// are the only ones that also cover the LDS-DMA ring in flight.
+constexpr int NST = 16;  // store instructions per wave per chunk
+constexpr int OOB = 0x7FFFFFFC;
+
+template <int EPI>
+__device__ __forceinline__ void rows_epilogue(const GemmParams& p, __amdgpu_buffer_rsrc_t cbuf, int m0, int n0,
+                                              const floatx16& acc, int r, int h, const float* __restrict__ bias_s,
+                                              const float4* __restrict__ qp_s, int cfirst) {
+    const int col = n0 + r;
+    const bool col_ok = col < p.N;
+    const int lc = col - cfirst;  // column in the group's LDS tables
+    const float bv = p.bias ? bias_s[lc] : 0.0f;
+    float4 qc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.qp) qc = qp_s[lc];
+    if constexpr (EPI == VASR_EPI_ARGMAX) {
+        const int slot = n0 / 32;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            float v = acc[i];
+            if (p.bias) v = v + bv;
+            if (p.qp) v = fake_quant(v, qc);
+            const unsigned u = __float_as_uint(v);
+            const unsigned ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+            const unsigned long long k0 = col_ok ? ((unsigned long long)ord << 32) | (0xFFFFFFFFu - (unsigned)col) : 0ull;
+            const unsigned long long key = gemm::max_u64_over_32_lanes(k0);  // lanes r = 16..31 hold it
+            const int off = (r == 31 && row < p.M) ? (row * (int)p.ldc + slot) * 8 : OOB;
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 kv = {(unsigned)key, (unsigned)(key >> 32)};
+            if (!(VASR_ROWS_ABLATE & 2)) __builtin_amdgcn_raw_buffer_store_b64(kv, cbuf, off, 0, VASR_ROWS_STORE_AUX);
+        }
+        return;
+    }
+    const bool sp = EPI == VASR_EPI_SOFTPLUS_FROM && col >= p.n_out;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const bool ok = col_ok && row < p.M;
+        float v = acc[i];
+        if (p.bias) v = v + bv;
+        if (p.qp) v = fake_quant(v, qc);
+        if constexpr (EPI == VASR_EPI_GELU) {
+            v = gelu_fast(v);
+        } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
+            v = sp ? softplus20_fast(v) : v;
+        } else if constexpr (EPI == VASR_EPI_RESIDUAL) {
+            v = v + p.aux[(int64_t)min(row, p.M - 1) * p.ld_aux + min(col, p.N - 1)];
+        } else if constexpr (EPI == VASR_EPI_GELU_PE) {
+            v = gelu_fast(v) + p.aux[(int64_t)min(row, p.M - 1) * p.ld_aux + min(col, p.N - 1)];
+        }
+        if (!(VASR_ROWS_ABLATE & 2))
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), cbuf, ok ? (row * (int)p.ldc + col) * 4 : OOB, 0,
+                                                  VASR_ROWS_STORE_AUX);
+    }
+}
+
+template <int KS, int EPI>
+__global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int n_groups, int chunks_per_group) {
+    constexpr int CHUNK = KS * 3 * 1024;       // one 32-column W chunk: [KS][3 planes][64 lanes][16 B]
+    constexpr int DW = 4;                      // loader waves (the first four) issue the chunk's DMA
+    constexpr int NDMA = 3 * KS / DW;          // LDS-DMA instructions per loader wave per chunk
+    static_assert((3 * KS) % DW == 0 && RW % DW == 0, "whole DMA pieces per loader wave");
+    __shared__ __attribute__((aligned(16))) char wb0[CHUNK];
+    __shared__ __attribute__((aligned(16))) char wb1[CHUNK];
+    __shared__ __attribute__((aligned(16))) char wb2[CHUNK];
+    __shared__ __attribute__((aligned(16))) char wb3[NSLOT > 3 ? CHUNK : 16];
+    __shared__ float bias_s[MAX_GROUP * 32];
+    __shared__ float4 qp_s[MAX_GROUP * 32];
+
+    const int nblk = (int)gridDim.x;
+    const int id = blockIdx.x;
+    const int q8 = nblk / 8, r8 = nblk % 8, xg = id % 8;
+    const int w = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + id / 8;
+    const int rb = w / n_groups, ng = w - rb * n_groups;
+    const int NT = (p.N + 31) / 32;
+    const int c0 = ng * chunks_per_group;
+    const int nc = min(chunks_per_group, NT - c0);
+    if (nc <= 0) return;  // block-uniform
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const int m0 = rb * 32 * RW + wave * 32;  // this wave's rows
+    const int cfirst = c0 * 32;
+
+    // A rows (lane (r, h): row r, k = 16 ks + 8 h + 0..7; columns past K read as 0 from a
+    // clamped address, no branches) and the group's epilogue tables
+    const float* __restrict__ arow = p.A + (int64_t)min(m0 + r, p.M - 1) * p.lda;
+    float4 xa[KS][2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = 16 * ks + 8 * h + 4 * u;
+            const float4 v = *reinterpret_cast<const float4*>(arow + min(k, p.K - 4));
+            xa[ks][u] = k < p.K ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    for (int i = tid; i < nc * 32; i += 64 * RW) {
+        const int col = min(cfirst + i, p.N - 1);
+        if (p.bias) bias_s[i] = p.bias[col];
+        if (p.qp) qp_s[i] = p.qp[col];
+    }
+    bf16x8 a[KS][3];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) split8(xa[ks][0], xa[ks][1], a[ks][0], a[ks][1], a[ks][2]);
+
+    const char* __restrict__ Wx = reinterpret_cast<const char*>(p.Wx);
+    auto slot = [&](int i) -> char* { return i == 0 ? wb0 : i == 1 ? wb1 : i == 2 ? wb2 : wb3; };
+    const bool loader = wave_u < DW;
+    auto issue = [&](int j) {
+        if (!loader) return;
+        const char* src = Wx + (int64_t)(c0 + j) * CHUNK + lane * 16;
+        char* dst = slot(j % NSLOT);
+#pragma unroll
+        for (int i = 0; i < NDMA; ++i) {
+            const int piece = i * DW + wave_u;
+            glds16(src + piece * 1024, dst + piece * 1024);
+        }
+    };
+    for (int j = 0; j < DEPTH && j < nc; ++j) issue(j);
+
+    // C as a raw buffer over its valid bytes (the host checks they fit 31 bits)
+    const int c_bytes = (EPI == VASR_EPI_ARGMAX ? 8 : 4) * ((p.M - 1) * (int)p.ldc + (EPI == VASR_EPI_ARGMAX ? NT : p.N));
+    const __amdgpu_buffer_rsrc_t cbuf = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, c_bytes, 0x00020000);
+    // accumulators: two sets of SUPER chunk tiles; a set's SUPER epilogues run back to back (so a
+    // row's SUPER x 128 B of C go out together) while the other set accumulates
+    floatx16 acc[2][SUPER];
+    auto epi_group = [&](auto Sc, int g, int n) {  // the n <= SUPER tiles of group g from set S
+        constexpr int S = decltype(Sc)::value;
+#pragma unroll
+        for (int t = 0; t < SUPER; ++t)
+            if (t < n) rows_epilogue<EPI>(p, cbuf, m0, (c0 + g * SUPER + t) * 32, acc[S][t], r, h, bias_s, qp_s, cfirst);
+    };
+    // store instructions this wave issues at step k: the whole previous group's at a group's first step
+    auto stores_at = [&](int k) { return (k % SUPER == 0 && k >= SUPER) ? NST * SUPER : 0; };
+    // chunk j (tile T of group j / SUPER, set S): wait for its DMA (counted: younger DMAs and
+    // stores stay in flight), publish it block-wide (the barrier also certifies every wave is done
+    // with the slot DMA(j + DEPTH) refills), drain the previous group at a group's first chunk,
+    // prefetch chunk j + DEPTH, then chunk j's MFMAs
+    auto step = [&](auto Sc, auto Tc, int j) {
+        constexpr int S = decltype(Sc)::value;
+        constexpr int T = decltype(Tc)::value;
+        // vector-memory ops this wave issued after DMA(j): the DMAs of chunks j + 1 .. j + DEPTH - 1
+        // and the epilogue stores of the steps after the one that issued DMA(j) (step j - DEPTH,
+        // or the prologue); older stores must have retired, younger ones stay in flight
+        int n_vm = 0;
+        if (loader && !((VASR_ROWS_ABLATE & 4) && j >= 1)) n_vm = (min(j + DEPTH - 1, nc - 1) - j) * NDMA;
+        if (!(VASR_ROWS_ABLATE & 2))
+            for (int k = max(j - DEPTH + 1, 0); k < j; ++k) n_vm += stores_at(k);
+        wait_vmcnt_rt(min(n_vm, 63));
+        if (!(VASR_ROWS_ABLATE & 8)) __builtin_amdgcn_s_barrier();
+        const char* wb = slot((VASR_ROWS_ABLATE & 4) ? min(j, DEPTH - 1) : j % NSLOT) + lane * 16;
+        // W fragments of k-step 0 first, so the chunk's first MFMA does not wait behind the epilogue
+        bf16x8 wf[2][3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) wf[0][pl] = *reinterpret_cast<const bf16x8*>(wb + pl * 1024);
+        if (T == 0 && j >= SUPER) epi_group(std::integral_constant<int, S ^ 1>(), j / SUPER - 1, SUPER);
+        if (j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
+        floatx16 c;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int cur = ks & 1;
+            if (ks + 1 < KS) {  // next k-step's fragments one step ahead of their MFMAs
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    wf[cur ^ 1][pl] = *reinterpret_cast<const bf16x8*>(wb + ((ks + 1) * 3 + pl) * 1024);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (VASR_ROWS_ABLATE & 1) {
+                c[0] += (float)a[ks][0][0] * (float)wf[cur][0][0] + (float)a[ks][2][1] * (float)wf[cur][2][1];
+                continue;
+            }
+            // small terms first, then the leading hi*hi term (gemm_x3.hip's order)
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][2], wf[cur][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0], wf[cur][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][1], wf[cur][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][1], wf[cur][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0], wf[cur][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0], wf[cur][0], c, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        acc[S][T] = c;
+    };
+    auto group = [&](auto Sc, int j0) {  // the chunks of one group, tiles 0 .. SUPER-1
+        step(Sc, std::integral_constant<int, 0>(), j0);
+        if constexpr (SUPER > 1) if (j0 + 1 < nc) step(Sc, std::integral_constant<int, 1>(), j0 + 1);
+        if constexpr (SUPER > 2) if (j0 + 2 < nc) step(Sc, std::integral_constant<int, 2>(), j0 + 2);
+        if constexpr (SUPER > 3) if (j0 + 3 < nc) step(Sc, std::integral_constant<int, 3>(), j0 + 3);
+    };
+    for (int j = 0; j < nc; j += 2 * SUPER) {
+        group(std::integral_constant<int, 0>(), j);
+        if (j + SUPER < nc) group(std::integral_constant<int, 1>(), j + SUPER);
+    }
+    const int gl = (nc - 1) / SUPER;  // the last group, drained here
+    if (gl & 1) epi_group(std::integral_constant<int, 1>(), gl, nc - gl * SUPER);
+    else epi_group(std::integral_constant<int, 0>(), gl, nc - gl * SUPER);
+}
+
+template <int KS>
+int launch_rows(const GemmParams& p, int epi, hipStream_t s) {
+    const int NT = (p.N + 31) / 32;
+    const int row_blocks = (p.M + 32 * RW - 1) / (32 * RW);
+    // column groups: at most one block per CU (LDS: NSLOT x 36 KiB per block), so the grid is a
+    // single round -- a second, partial round costs as much as the first
+    int groups = row_blocks >= kCUs ? 1 : kCUs / row_blocks;
+    groups = max(1, min(groups, NT));
+    const int per = min((NT + groups - 1) / groups, MAX_GROUP);
+    groups = (NT + per - 1) / per;
+    const dim3 grid(row_blocks * groups), block(64 * RW);
+#define VASR_R(E) hipLaunchKernelGGL((gemm_rows_kernel<KS, E>), grid, block, 0, s, p, groups, per)
+    switch (epi) {
+        case VASR_EPI_NONE: VASR_R(VASR_EPI_NONE); break;
+        case VASR_EPI_GELU: VASR_R(VASR_EPI_GELU); break;
+        case VASR_EPI_SOFTPLUS_FROM: VASR_R(VASR_EPI_SOFTPLUS_FROM); break;
+        case VASR_EPI_RESIDUAL: VASR_R(VASR_EPI_RESIDUAL); break;
+        case VASR_EPI_GELU_PE: VASR_R(VASR_EPI_GELU_PE); break;
+        case VASR_EPI_ARGMAX: VASR_R(VASR_EPI_ARGMAX); break;
+        default: set_error("vasr_linear_x3_f32: rows engine: epilogue %d not supported", epi); return VASR_EINVAL;
+    }
+#undef VASR_R
+    return launch_status("vasr_linear_x3_f32");
+}
+
+}  // namespace
+
+// The rows engine serves batch-1 launches with K <= 192 and unpaired epilogues (the model's
+// projection GEMMs at K = 192, the CTC head); returns false when the tile kernel should run.
+bool try_rows_x3(const GemmParams& p, int batch, int epi, hipStream_t s, int* rc) {
+    if (batch != 1 || p.Kp > 192 || p.M <= 0 || epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION) return false;
+    if (p.Kp != 128 && p.Kp != 192) return false;  // the W chunk stride is Kp / 16 k-steps
+    // raw-buffer C addressing: the valid bytes must fit the 31-bit offsets
+    if ((int64_t)p.M * p.ldc * (epi == VASR_EPI_ARGMAX ? 8 : 4) >= ((int64_t)1 << 31) - 64) return false;
+    const int engine = option(VASR_OPT_GEMM_ENGINE);  // 0 auto, 1 tiles, 2 rows
+    if (engine == 1) return false;
+    // auto: the rows engine where it measured faster (profiles/r03l: K = 192, N >= 512 -- the
+    // composed head GEMM 35.8 vs 45.6 us, in_proj 21.1 vs 22.8; at N = 384 / 192 a block's short
+    // chunk run does not amortise its A load); the argmax head keeps the tiles (its per-chunk
+    // 32-lane reductions), and so do the residual / GELU+PE epilogues (they spill at 8 waves)
+    if (engine == 0 && (p.Kp != 192 || p.N < 512 ||
+                        !(epi == VASR_EPI_NONE || epi == VASR_EPI_GELU || epi == VASR_EPI_SOFTPLUS_FROM)))
+        return false;
+    *rc = p.Kp == 128 ? launch_rows<8>(p, epi, s) : launch_rows<12>(p, epi, s);
+    return true;
+}
+
+}  // namespace vasr

@@ -465,6 +465,8 @@ VASR_API int vasr_linear_x3_f32(const vasr_gemm_args* a, const uint16_t* w_split
     const int epi = a->epilogue;
     const bool pair = epi == VASR_EPI_PAIR_POWER || epi == VASR_EPI_PAIR_FUSION;
     hipStream_t s = as_stream(stream);
+    int rc;
+    if (try_rows_x3(p, a->batch, epi, s, &rc)) return rc;
 #ifdef VASR_X3_FORCE_CFG
     const int cfg = VASR_X3_FORCE_CFG;  // diagnostic builds only
 #else

@@ -43,7 +43,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef VASR_SCAN_ABLATE
 #define VASR_SCAN_ABLATE 0  // diagnostic builds only (tools/scan_ablate.sh): 1 no exp,
 #endif                      // 4 no B/C LDS reads, 8 no chunk staging after the first,
-                            // 16 no tree update, 32 no gated-output pass
+                            // 16 no tree update, 32 no gated-output pass, 64 no block barriers
 #ifndef VASR_SCAN_WAVES
 #define VASR_SCAN_WAVES 3   // waves per SIMD the register allocator targets
 #endif
