@@ -49,8 +49,9 @@ enum vasr_option {
     VASR_OPT_SCAN_LANES = 0, /* state indices per lane of vasr_ssm_scan_f32: 0, 2, 4 (VASR_SCAN_NPL)       */
     VASR_OPT_SCAN_CHUNK = 1, /* time steps per staged chunk of the streaming scan: 0, 16, 32 (VASR_SCAN_T) */
     VASR_OPT_TAIL_ROWS = 2,  /* token rows per fused-SSMBlock-tail workgroup: 0, 16, 32 (VASR_TAIL_ROWS)   */
-    VASR_OPT_GEMM_ENGINE = 3 /* split-bf16 GEMM main loop: 0 auto, 1 LDS-ring tiles, 2 A-rows-stationary
-                                (K = 128 / 192, batch 1, unpaired epilogues) (VASR_GEMM_ENGINE)          */
+    VASR_OPT_GEMM_ENGINE = 3, /* split-bf16 GEMM main loop: 0 auto, 1 LDS-ring tiles, 2 A-rows-stationary
+                                 (K = 128 / 192, batch 1, unpaired epilogues) (VASR_GEMM_ENGINE)         */
+    VASR_OPT_TAIL_WAVES = 4   /* waves per fused-SSMBlock-tail workgroup: 0, 4, 6, 12 (VASR_TAIL_WAVES)    */
 };
 int vasr_set_option(int key, int value);
 

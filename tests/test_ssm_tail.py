@@ -64,18 +64,20 @@ def test_tail_matches_fp64(M):
 
 @pytest.mark.parametrize("M", [17, 501, 4097])
 def test_tail_row_forms_bitwise_equal(M):
-    """16- and 32-row workgroups (VASR_OPT_TAIL_ROWS; the default takes 16 up to M = 4096) perform
-    the same float operations per element: outputs are bitwise equal."""
+    """16- and 32-row workgroups (VASR_OPT_TAIL_ROWS; the default takes 16 up to M = 4096) of 4, 6
+    or 12 waves (VASR_OPT_TAIL_WAVES: 3, 2 or 1 output column tiles per wave) perform the same
+    float operations per element: outputs are bitwise equal."""
     from velocity_asr import _lib, ops
     rng = np.random.default_rng(M + 1)
     P = _params(9)
     g = rng.standard_normal((M, 384)).astype(np.float32)
     x = rng.standard_normal((M, 192)).astype(np.float32)
-    with ops.option(_lib.OPT_TAIL_ROWS, 16):
+    with ops.option(_lib.OPT_TAIL_ROWS, 16), ops.option(_lib.OPT_TAIL_WAVES, 4):
         a = _run(g, x, P)
-    with ops.option(_lib.OPT_TAIL_ROWS, 32):
-        b = _run(g, x, P)
-    np.testing.assert_array_equal(a, b)
+    for rows in (16, 32):
+        for waves in (4, 6, 12):
+            with ops.option(_lib.OPT_TAIL_ROWS, rows), ops.option(_lib.OPT_TAIL_WAVES, waves):
+                np.testing.assert_array_equal(_run(g, x, P), a, err_msg=f"rows {rows} waves {waves}")
 
 
 def test_tail_strided_input():

@@ -1,5 +1,6 @@
 """Fused SSMBlock tail vs the unfused launches it replaces, isolated, at the bench's launch
-shapes (M = 8016 and 16032 token rows).  Usage (GPU box): python tools/tail_bench.py"""
+shapes (M = 8016 and 16032 token rows), and its workgroup forms (VASR_OPT_TAIL_ROWS x
+VASR_OPT_TAIL_WAVES).  Usage (GPU box): python tools/tail_bench.py [M ...]"""
 import os
 import sys
 
@@ -39,8 +40,16 @@ def main():
             f = ops.gemm(x1, w1, b1, epilogue=_lib.EPI_GELU, ln=(lw, lb, 1e-5))
             return ops.gemm(f, w2, b2, epilogue=_lib.EPI_RESIDUAL, aux=x1)
         tf, tp = timed(fused), timed(plain)
-        err = (fused() - plain()).abs().max().item()
+        ref = fused()
+        err = (ref - plain()).abs().max().item()
         print(f"M={M}: fused tail {tf:.1f} us, unfused (3 GEMMs + LN) {tp:.1f} us, max |diff| {err:.2e}", flush=True)
+        # workgroup forms (rows x waves): same arithmetic per output, bitwise equal
+        for rows in (16, 32):
+            for waves in (4, 6, 12):
+                with ops.option(_lib.OPT_TAIL_ROWS, rows), ops.option(_lib.OPT_TAIL_WAVES, waves):
+                    t = timed(fused)
+                    same = torch.equal(fused(), ref)
+                print(f"M={M}: rows {rows} waves {waves:2d}: {t:6.1f} us{'' if same else '  MISMATCH'}", flush=True)
 
 
 if __name__ == "__main__":

@@ -28,15 +28,16 @@ VASR_API const char* vasr_last_error(void) { return vasr::g_last_error; }
 
 // Tuning options (vasr_set_option): process-wide, defaults from the environment read once.
 namespace {
-constexpr int kNumOptions = 4;
-const char* const kOptionEnv[kNumOptions] = {"VASR_SCAN_NPL", "VASR_SCAN_T", "VASR_TAIL_ROWS", "VASR_GEMM_ENGINE"};
-const int kOptionValues[kNumOptions][3] = {{0, 2, 4}, {0, 16, 32}, {0, 16, 32}, {0, 1, 2}};
+constexpr int kNumOptions = 5;
+const char* const kOptionEnv[kNumOptions] = {"VASR_SCAN_NPL", "VASR_SCAN_T", "VASR_TAIL_ROWS", "VASR_GEMM_ENGINE",
+                                               "VASR_TAIL_WAVES"};
+const int kOptionValues[kNumOptions][4] = {{0, 2, 4, -1}, {0, 16, 32, -1}, {0, 16, 32, -1}, {0, 1, 2, -1}, {0, 4, 6, 12}};
 std::atomic<int> g_options[kNumOptions];
 std::once_flag g_options_once;
 
 bool option_value_ok(int key, int v) {
     for (int a : kOptionValues[key])
-        if (v == a) return true;
+        if (a >= 0 && v == a) return true;
     return false;
 }
 

@@ -328,9 +328,10 @@ bool try_rows_x3(const GemmParams& p, int batch, int epi, hipStream_t s, int* rc
     if (engine == 1) return false;
     // auto: the rows engine where it measured faster (profiles/r03l: K = 192, N >= 512 -- the
     // composed head GEMM 35.8 vs 45.6 us, in_proj 21.1 vs 22.8; at N = 384 / 192 a block's short
-    // chunk run does not amortise its A load); the argmax head keeps the tiles (its per-chunk
+    // chunk run does not amortise its A load; one utterance, M = 501: 13.2 vs 8.4 us in the
+    // graph, profiles/r03m -- two 256-row blocks per column group); the argmax head keeps the tiles (its per-chunk
     // 32-lane reductions), and so do the residual / GELU+PE epilogues (they spill at 8 waves)
-    if (engine == 0 && (p.Kp != 192 || p.N < 512 ||
+    if (engine == 0 && (p.Kp != 192 || p.N < 512 || p.M < 4096 ||
                         !(epi == VASR_EPI_NONE || epi == VASR_EPI_GELU || epi == VASR_EPI_SOFTPLUS_FROM)))
         return false;
     *rc = p.Kp == 128 ? launch_rows<8>(p, epi, s) : launch_rows<12>(p, epi, s);

@@ -1,7 +1,6 @@
-// Pieces shared by the fused SSMBlock kernels (ssm_tail.hip: out_proj -> LN2 -> FFN;
-// ssm_head.hip: LN1 + causal dwconv -> in_proj -> [x_proj; dt_proj]): 32 token rows per
-// workgroup, four waves, A operands as bf16 planes in LDS (split once per block), weights
-// streamed global -> VGPRs in the v_mfma_f32_16x16x32_bf16 fragment layout.
+// Pieces of the fused SSMBlock tail kernel (ssm_tail.hip: out_proj -> LN2 -> FFN): A operands
+// as bf16 planes in LDS (split once per block), weights streamed global -> VGPRs in the
+// v_mfma_f32_16x16x32_bf16 fragment layout.
 #pragma once
 
 #include "gemm_split.h"
@@ -14,10 +13,6 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int TD = 192;          // d_model
 constexpr int TE = 384;          // FFN width = d_inner
-constexpr int TBM = 32;          // token rows per workgroup
-constexpr int TWAVES = 4;
-constexpr int PLANE_E = TBM * TE * 2;  // one bf16 plane of a 384-wide A tile (24 KiB)
-constexpr int PLANE_D = TBM * TD * 2;  // one bf16 plane of a 192-wide A tile (12 KiB)
 
 // byte offset of bf16 element (r, col) in one plane: 8-element (16-B) chunks, chunk c of row r
 // at c ^ (r & 15) (384-wide) or c ^ (r & 7) (192-wide): conflict-free ds_read_b128 fragment
@@ -81,7 +76,7 @@ __device__ __forceinline__ floatx4 mac_tile(const bf16x8 (&a)[NP], const bf16x8 
 
 // the A fragment of one 16-row tile for a 32-k step: NP chunks of the plane image at `base`
 // (planes of ROWS rows)
-template <int NP, int WIDTH, int ROWS = TBM>
+template <int NP, int WIDTH, int ROWS>
 __device__ __forceinline__ void read_a(const char* base, int row, int ks, int q, bf16x8 (&a)[NP]) {
     constexpr int SW = WIDTH == TE ? 15 : 7;
     constexpr int PB = ROWS * WIDTH * 2;

@@ -49,8 +49,16 @@ constexpr int NSTAGES = 36;      // out_proj 12 k-steps, FFN1 2 halves x 6, FFN2
 #ifndef VASR_TAIL_PD16
 #define VASR_TAIL_PD16 2  // the 16-row form (two waves per SIMD: 256 registers, no spills at 2)
 #endif
-template <int NP, int RT = 2>
-constexpr int pd_of() { return NP == 3 ? (RT == 1 ? VASR_TAIL_PD16 : VASR_TAIL_PD) : 6; }
+#ifndef VASR_TAIL_PD12
+#define VASR_TAIL_PD12 6  // 12 waves (one column tile each), 16 rows: 168 registers, no spills
+#endif
+template <int NP, int RT = 2, int CT = 3>
+constexpr int pd_of() {
+    if constexpr (NP == 1) return CT == 3 ? 6 : 8;
+    if constexpr (CT == 1) return RT == 1 ? VASR_TAIL_PD12 : 4;
+    if constexpr (CT == 2) return 3;
+    return RT == 1 ? VASR_TAIL_PD16 : VASR_TAIL_PD;
+}
 
 struct TailParams {
     const float* g;
@@ -71,10 +79,14 @@ struct TailParams {
 };
 
 // RT = 16-row tiles per workgroup: 2 (32 rows, one block per CU) or 1 (16 rows, half the LDS,
-// two blocks per CU: twice the weight stream per row, two waves per SIMD to hide it)
-template <int NP, int RT>
+// two blocks per CU: twice the weight stream per row, two waves per SIMD to hide it).
+// CT = 16-column output tiles per wave: 3 (4 waves), or 2 / 1 (6 / 12 waves: the block's
+// weight stream split over more waves, each with a deeper prefetch -- the small-M forms, where
+// one block per CU leaves the registers for it)
+template <int NP, int RT, int CT = 3>
 struct TailCtx {
-    static constexpr int PD = pd_of<NP, RT>();
+    static constexpr int NWV = 12 / CT;  // waves per workgroup
+    static constexpr int PD = pd_of<NP, RT, CT>();
     static constexpr int RING = PD + 1;
     static constexpr int ROWS = 16 * RT;
     static constexpr int PE = ROWS * TE * 2;  // one bf16 plane of a 384-wide A tile
@@ -83,16 +95,16 @@ struct TailCtx {
     char* R;   // 384-wide planes (g, f) / fp32 x1 scratch
     char* H;   // 192-wide planes (h)
     int lane, wave, r, q, m0;
-    floatx4 acc[RT][3];
-    bf16x8 w[RING][3][NP];  // [ring slot][column tile][plane]
-    float x1[RT][3][4];     // residual x, then x1 = out_proj(g) + x
-    float bb1[2][3], bb2[3], lnw[3], lnb[3];
+    floatx4 acc[RT][CT];
+    bf16x8 w[RING][CT][NP];  // [ring slot][column tile][plane]
+    float x1[RT][CT][4];     // residual x, then x1 = out_proj(g) + x
+    float bb1[2][CT], bb2[CT], lnw[3], lnb[3];
 };
 
-// weight fragments of step S for this wave: column tiles 3w .. 3w+2, NP planes, from the
+// weight fragments of step S for this wave: column tiles CT w .. CT w + CT - 1, NP planes, from the
 // fragment layout [N/16][K/32][NP][64][8]
-template <int S, int NP, int RT>
-__device__ __forceinline__ void load_w(TailCtx<NP, RT>& c) {
+template <int S, int NP, int RT, int CT>
+__device__ __forceinline__ void load_w(TailCtx<NP, RT, CT>& c) {
     const uint16_t* W;
     int nt0, ks, KS;
     if constexpr (S < 12) {
@@ -103,27 +115,27 @@ __device__ __forceinline__ void load_w(TailCtx<NP, RT>& c) {
         W = c.P.w2, nt0 = 0, ks = S - 24, KS = TE / 32;
     }
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-        const int nt = nt0 + 3 * c.wave + t;
+    for (int t = 0; t < CT; ++t) {
+        const int nt = nt0 + CT * c.wave + t;
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl)
-            c.w[S % TailCtx<NP, RT>::RING][t][pl] =
+            c.w[S % TailCtx<NP, RT, CT>::RING][t][pl] =
                 *reinterpret_cast<const bf16x8*>(W + ((int64_t)(nt * KS + ks) * NP + pl) * 512 + c.lane * 8);
     }
 }
 
 // the first PD steps' weights (prologue)
-template <int S, int NP, int RT>
-__device__ __forceinline__ void load_first(TailCtx<NP, RT>& c) {
-    load_w<S, NP, RT>(c);
-    if constexpr (S + 1 < TailCtx<NP, RT>::PD) load_first<S + 1, NP, RT>(c);
+template <int S, int NP, int RT, int CT>
+__device__ __forceinline__ void load_first(TailCtx<NP, RT, CT>& c) {
+    load_w<S, NP, RT, CT>(c);
+    if constexpr (S + 1 < TailCtx<NP, RT, CT>::PD) load_first<S + 1, NP, RT, CT>(c);
 }
 
-template <int S, int NP, int RT>
-__device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
-    using Ctx = TailCtx<NP, RT>;
+template <int S, int NP, int RT, int CT>
+__device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
+    using Ctx = TailCtx<NP, RT, CT>;
     constexpr int PD = Ctx::PD;
-    if constexpr (S + PD < NSTAGES) load_w<S + PD, NP, RT>(c);
+    if constexpr (S + PD < NSTAGES) load_w<S + PD, NP, RT, CT>(c);
     // keep the prefetch where it is: without this fence the scheduler sinks the loads next to
     // their use (to save registers) and the step then waits on them (measured: the weight
     // stream then ran at a third of the L2 rate)
@@ -140,7 +152,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
 #pragma unroll
     for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % Ctx::RING][t], c.acc[tm][t]);
+        for (int t = 0; t < CT; ++t) c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % Ctx::RING][t], c.acc[tm][t]);
 
     if constexpr (S == 11) {
         // x1 = out_proj(g) + x (registers, kept for the final residual) -> fp32 scratch in R
@@ -150,8 +162,8 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
 #pragma unroll
         for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const int col = 16 * (3 * c.wave + t) + c.r;
+            for (int t = 0; t < CT; ++t) {
+                const int col = 16 * (CT * c.wave + t) + c.r;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     c.x1[tm][t][i] = c.acc[tm][t][i] + c.x1[tm][t][i];
@@ -162,9 +174,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
         lds_barrier();
         // h = LayerNorm_2(x1): one wave per row with vasr_layer_norm_f32's operations, each
         // value split into the three planes of H
-#pragma unroll
-        for (int k = 0; k < Ctx::ROWS / TWAVES; ++k) {
-            const int rr = Ctx::ROWS / TWAVES * c.wave + k;
+        for (int rr = c.wave; rr < Ctx::ROWS; rr += Ctx::NWV) {
             float v[3];
             float sum = 0.f;
 #pragma unroll
@@ -192,8 +202,8 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
 #pragma unroll
         for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-            for (int t = 0; t < 3; ++t) {
-                const int col = TD * hh + 16 * (3 * c.wave + t) + c.r;
+            for (int t = 0; t < CT; ++t) {
+                const int col = TD * hh + 16 * (CT * c.wave + t) + c.r;
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     split_store<NP>(c.R, Ctx::PE, poff<TE>(16 * tm + 4 * c.q + i, col),
@@ -202,12 +212,13 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT>& c) {
             }
         if constexpr (S == 23) lds_barrier();  // f complete before FFN2 reads it
     }
-    if constexpr (S + 1 < NSTAGES) tail_step<S + 1, NP, RT>(c);
+    if constexpr (S + 1 < NSTAGES) tail_step<S + 1, NP, RT, CT>(c);
 }
 
-template <int NP, int RT>
-__global__ __launch_bounds__(256, RT == 1 ? 2 : 1) void ssm_tail_kernel(TailParams P) {
-    using Ctx = TailCtx<NP, RT>;
+template <int NP, int RT, int CT = 3>
+__global__ __launch_bounds__(64 * (12 / CT), RT == 1 && CT == 3 ? 2 : 1) void ssm_tail_kernel(TailParams P) {
+    using Ctx = TailCtx<NP, RT, CT>;
+    constexpr int NT = 64 * Ctx::NWV;  // threads
     __shared__ __attribute__((aligned(16))) char R[NP * Ctx::PE];
     __shared__ __attribute__((aligned(16))) char H[NP * Ctx::PDB];
     Ctx c{P, R, H};
@@ -218,12 +229,13 @@ __global__ __launch_bounds__(256, RT == 1 ? 2 : 1) void ssm_tail_kernel(TailPara
     c.m0 = blockIdx.x * Ctx::ROWS;
     // weights of the first PD steps, then the g tile (split once into R's planes), the residual
     // x and the epilogue constants: all of these loads are in flight together
-    load_first<0, NP, RT>(c);
+    load_first<0, NP, RT, CT>(c);
     __builtin_amdgcn_sched_barrier(0);
     constexpr int UNITS = Ctx::ROWS * TE / 8;  // 8-float chunks of the g tile
+    static_assert(UNITS % NT == 0, "whole g-tile staging rounds");
 #pragma unroll
-    for (int k = 0; k < UNITS / 256; ++k) {
-        const int u = threadIdx.x + 256 * k;
+    for (int k = 0; k < UNITS / NT; ++k) {
+        const int u = threadIdx.x + NT * k;
         const int rr = u / (TE / 8), ch = u - rr * (TE / 8);
         const float* src = P.g + (int64_t)min(c.m0 + rr, P.M - 1) * P.ldg + 8 * ch;
         const float4 v0 = *reinterpret_cast<const float4*>(src);
@@ -233,8 +245,8 @@ __global__ __launch_bounds__(256, RT == 1 ? 2 : 1) void ssm_tail_kernel(TailPara
 #pragma unroll
     for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const int col = 16 * (3 * c.wave + t) + c.r;
+        for (int t = 0; t < CT; ++t) {
+            const int col = 16 * (CT * c.wave + t) + c.r;
             c.bb2[t] = P.b2[col];
             c.bb1[0][t] = P.b1[col];
             c.bb1[1][t] = P.b1[TD + col];
@@ -251,13 +263,13 @@ __global__ __launch_bounds__(256, RT == 1 ? 2 : 1) void ssm_tail_kernel(TailPara
         c.lnb[i] = P.ln_b[c.lane + 64 * i];
     }
     lds_barrier();  // the g planes are complete
-    tail_step<0, NP, RT>(c);
+    tail_step<0, NP, RT, CT>(c);
     // out = ffn.3(f) + b2 + x1
 #pragma unroll
     for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const int col = 16 * (3 * c.wave + t) + c.r;
+        for (int t = 0; t < CT; ++t) {
+            const int col = 16 * (CT * c.wave + t) + c.r;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int row = c.m0 + 16 * tm + 4 * c.q + i;
@@ -320,6 +332,33 @@ int tail_rows(int M) {
     return M <= 4096 ? 16 : 32;  // 256 CUs x 16 rows
 }
 
+// Waves per workgroup (12 / column tiles per wave).  At 32 rows, 12 waves of one column tile
+// each take 23.3 vs 26.2 us at M = 8016 (profiles/r03m/tail.txt: the block's MFMA chain split
+// three ways per SIMD); 16-row blocks do not gain (18-19 us for any wave count: the per-CU L2
+// weight stream, 1.3 MB per block at ~70 GB/s, sets their time).  vasr_set_option(
+// VASR_OPT_TAIL_WAVES, 4|6|12) (env VASR_TAIL_WAVES) forces one.
+int tail_waves(int M) {
+    if (const int w = option(VASR_OPT_TAIL_WAVES)) return w;
+    return tail_rows(M) == 32 ? 12 : 4;
+}
+
+template <int NP>
+void launch_tail(const TailParams& p, hipStream_t s) {
+    const int rows = tail_rows(p.M), waves = tail_waves(p.M);
+    const dim3 grid((unsigned)((p.M + rows - 1) / rows)), block(64 * waves);
+#define VASR_T(RT, CT) hipLaunchKernelGGL((ssm_tail_kernel<NP, RT, CT>), grid, block, 0, s, p)
+    if (rows == 16) {
+        if (waves == 12) VASR_T(1, 1);
+        else if (waves == 6) VASR_T(1, 2);
+        else VASR_T(1, 3);
+    } else {
+        if (waves == 12) VASR_T(2, 1);
+        else if (waves == 6) VASR_T(2, 2);
+        else VASR_T(2, 3);
+    }
+#undef VASR_T
+}
+
 int tail_args(const float* g, int64_t ldg, const float* x, int64_t ldx, const uint16_t* wo, const float* ln_w,
               const float* ln_b, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2, float* out,
               int64_t ldo, int M, int D, int E, const char* fn) {
@@ -363,11 +402,8 @@ VASR_API int vasr_ssm_block_tail_bf16(const float* g, int64_t ldg, const float* 
                            "vasr_ssm_block_tail_bf16"))
         return rc;
     if (M == 0) return VASR_OK;
-    TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
-    if (tail_rows(M) == 16)
-        hipLaunchKernelGGL((ssm_tail_kernel<1, 1>), dim3((M + 15) / 16), dim3(64 * TWAVES), 0, as_stream(stream), p);
-    else
-        hipLaunchKernelGGL((ssm_tail_kernel<1, 2>), dim3((M + 31) / 32), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    const TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
+    launch_tail<1>(p, as_stream(stream));
     return launch_status("vasr_ssm_block_tail_bf16");
 }
 
@@ -397,10 +433,7 @@ VASR_API int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x
                            "vasr_ssm_block_tail_f32"))
         return rc;
     if (M == 0) return VASR_OK;
-    TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
-    if (tail_rows(M) == 16)
-        hipLaunchKernelGGL((ssm_tail_kernel<3, 1>), dim3((M + 15) / 16), dim3(64 * TWAVES), 0, as_stream(stream), p);
-    else
-        hipLaunchKernelGGL((ssm_tail_kernel<3, 2>), dim3((M + 31) / 32), dim3(64 * TWAVES), 0, as_stream(stream), p);
+    const TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
+    launch_tail<3>(p, as_stream(stream));
     return launch_status("vasr_ssm_block_tail_f32");
 }
