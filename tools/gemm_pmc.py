@@ -8,8 +8,8 @@ Shape sets:
   head (default)  the kernels the HEAD step runs: the composed
                   [in_proj; x_proj.dt_proj] GEMM (N 1280, K 192, softplus from column 768),
                   the CTC head with the fused argmax (N 1000), and the fused SSMBlock tail
-                  (ssm_tail_kernel: <3, 2> at M = 8016 and <3, 1> at the global blocks'
-                  M = 16 x 64 = 1024)
+                  (ssm_tail_kernel: 32 rows x 12 waves at M = 8016, 16 rows x 4 waves at the
+                  global blocks' M = 16 x 64 = 1024)
   split           the pre-composition projection GEMMs (round-2 table)
 Usage (GPU box): python tools/gemm_pmc.py [M] [head|split]"""
 import json
@@ -40,7 +40,10 @@ def main():
     order = []
     for name, N, K, epi, lda in (HEAD if which == "head" else SPLIT):
         m = 1024 if epi == "tail1024" else M
-        kernel = "gemm_x3_kernel"
+        # the engine the launcher picks (gemm_rows.hip try_rows_x3: K = 192, N >= 512, M >= 4096,
+        # unpaired non-argmax epilogues -> A-rows-stationary; else the LDS-ring tiles)
+        rows = K == 192 and N >= 512 and m >= 4096 and epi in ("none", "gelu", "softplus")
+        kernel = "gemm_rows_kernel" if rows else "gemm_x3_kernel"
         flops = 2.0 * m * N * K
         if epi.startswith("tail"):
             D, Ei = 192, 384

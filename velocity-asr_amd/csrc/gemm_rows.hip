@@ -63,6 +63,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int RW = VASR_ROWS_WAVES;  // waves per block (4: one per SIMD)
 constexpr int DEPTH = VASR_ROWS_DEPTH;
 constexpr int NSLOT = DEPTH + 1;
+#ifndef VASR_ROWS_ISSUE_FIRST
+#define VASR_ROWS_ISSUE_FIRST 0  // issue chunk j + DEPTH's LDS-DMA before chunk j - 1's epilogue stores
+#endif
+#ifndef VASR_ROWS_NOSTWAIT
+#define VASR_ROWS_NOSTWAIT 0  // waves with no DMA never wait for their stores
+#endif
 #ifndef VASR_ROWS_SUPER
 #define VASR_ROWS_SUPER 1  // chunks per store group (their epilogues run back to back)
 #endif
@@ -238,7 +244,8 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         int n_vm = 0;
         if (loader && !((VASR_ROWS_ABLATE & 4) && j >= 1)) n_vm = (min(j + DEPTH - 1, nc - 1) - j) * NDMA;
         if (!(VASR_ROWS_ABLATE & 2))
-            for (int k = max(j - DEPTH + 1, 0); k < j; ++k) n_vm += stores_at(k);
+            for (int k = max(j - DEPTH + (VASR_ROWS_ISSUE_FIRST ? 0 : 1), 0); k < j; ++k) n_vm += stores_at(k);
+        if (VASR_ROWS_NOSTWAIT && !loader) n_vm = 63;  // no DMA to wait for: stores stay in flight
         wait_vmcnt_rt(min(n_vm, 63));
         if (!(VASR_ROWS_ABLATE & 8)) __builtin_amdgcn_s_barrier();
         const char* wb = slot((VASR_ROWS_ABLATE & 4) ? min(j, DEPTH - 1) : j % NSLOT) + lane * 16;
@@ -246,8 +253,9 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         bf16x8 wf[2][3];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) wf[0][pl] = *reinterpret_cast<const bf16x8*>(wb + pl * 1024);
+        if (VASR_ROWS_ISSUE_FIRST && j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
         if (T == 0 && j >= SUPER) epi_group(std::integral_constant<int, S ^ 1>(), j / SUPER - 1, SUPER);
-        if (j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
+        if (!VASR_ROWS_ISSUE_FIRST && j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
         floatx16 c;
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = 0.f;
