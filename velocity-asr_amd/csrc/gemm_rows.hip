@@ -17,8 +17,11 @@
 // column groups (runs of chunks), at most one block per CU so the grid is one round; blocks id,
 // id + 8, ... share an XCD and get consecutive (row block, column group) items, so the column
 // groups of one row block read its A rows from one L2.  Epilogues: gemm_common.h's (unpaired
-// ones), per 32 x 32 chunk.  Measured variants (profiles/r03k): 4 waves per block, cached
-// stores, and store groups of 2-4 chunks (VASR_ROWS_SUPER) were all slower or equal.
+// ones), per 32 x 32 chunk.  Measured variants, all slower or equal: 4 waves per
+// block, cached stores, store groups of 2-4 chunks written back to back (profiles/r03k), the
+// chunk's DMA issued before the previous epilogue / no store waits in non-loader waves
+// (profiles/r03r), and the epilogue interleaved into the next chunk's k-steps at 4 or 8 waves
+// (37.0 / 37.6 vs 33.4 us, profiles/r03u).
 #include <type_traits>
 
 #include "gemm_common.h"
@@ -63,18 +66,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int RW = VASR_ROWS_WAVES;  // waves per block (4: one per SIMD)
 constexpr int DEPTH = VASR_ROWS_DEPTH;
 constexpr int NSLOT = DEPTH + 1;
-#ifndef VASR_ROWS_ISSUE_FIRST
-#define VASR_ROWS_ISSUE_FIRST 0  // issue chunk j + DEPTH's LDS-DMA before chunk j - 1's epilogue stores
+#ifndef VASR_ROWS_MAX_GROUP
+#define VASR_ROWS_MAX_GROUP 16
 #endif
-#ifndef VASR_ROWS_NOSTWAIT
-#define VASR_ROWS_NOSTWAIT 0  // waves with no DMA never wait for their stores
-#endif
-#ifndef VASR_ROWS_SUPER
-#define VASR_ROWS_SUPER 1  // chunks per store group (their epilogues run back to back)
-#endif
-constexpr int SUPER = VASR_ROWS_SUPER;
-static_assert(SUPER >= 1 && SUPER <= 4, "store group of 1..4 chunks");
-constexpr int MAX_GROUP = 40;   // chunks per column group (LDS epilogue tables: 40 x 32 columns)
+constexpr int MAX_GROUP = VASR_ROWS_MAX_GROUP;  // chunks per column group (LDS epilogue tables: MAX_GROUP x 32 columns)
 
 // s_waitcnt vmcnt(n) for a runtime n in [0, 63] (the immediate has to be a constant)
 __device__ __forceinline__ void wait_vmcnt_rt(int n) {
@@ -127,26 +122,40 @@ __device__ __forceinline__ void rows_epilogue(const GemmParams& p, __amdgpu_buff
         }
         return;
     }
-    const bool sp = EPI == VASR_EPI_SOFTPLUS_FROM && col >= p.n_out;
+    // SP: 0 no softplus, 1 every column of the chunk, 2 per column (the chunk straddles n_out)
+    auto body = [&](auto SPc) {
+        constexpr int SP = decltype(SPc)::value;
+        const bool sp = SP == 1 || (SP == 2 && col >= p.n_out);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const bool ok = col_ok && row < p.M;
-        float v = acc[i];
-        if (p.bias) v = v + bv;
-        if (p.qp) v = fake_quant(v, qc);
-        if constexpr (EPI == VASR_EPI_GELU) {
-            v = gelu_fast(v);
-        } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
-            v = sp ? softplus20_fast(v) : v;
-        } else if constexpr (EPI == VASR_EPI_RESIDUAL) {
-            v = v + p.aux[(int64_t)min(row, p.M - 1) * p.ld_aux + min(col, p.N - 1)];
-        } else if constexpr (EPI == VASR_EPI_GELU_PE) {
-            v = gelu_fast(v) + p.aux[(int64_t)min(row, p.M - 1) * p.ld_aux + min(col, p.N - 1)];
+        for (int i = 0; i < 16; ++i) {
+            const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const bool ok = col_ok && row < p.M;
+            float v = acc[i];
+            if (p.bias) v = v + bv;
+            if (p.qp) v = fake_quant(v, qc);
+            if constexpr (EPI == VASR_EPI_GELU) {
+                v = gelu_fast(v);
+            } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
+                if constexpr (SP == 1) v = softplus20_fast(v);
+                else if constexpr (SP == 2) v = sp ? softplus20_fast(v) : v;
+            } else if constexpr (EPI == VASR_EPI_RESIDUAL) {
+                v = v + p.aux[(int64_t)min(row, p.M - 1) * p.ld_aux + min(col, p.N - 1)];
+            } else if constexpr (EPI == VASR_EPI_GELU_PE) {
+                v = gelu_fast(v) + p.aux[(int64_t)min(row, p.M - 1) * p.ld_aux + min(col, p.N - 1)];
+            }
+            if (!(VASR_ROWS_ABLATE & 2))
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), cbuf, ok ? (row * (int)p.ldc + col) * 4 : OOB,
+                                                      0, VASR_ROWS_STORE_AUX);
         }
-        if (!(VASR_ROWS_ABLATE & 2))
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), cbuf, ok ? (row * (int)p.ldc + col) * 4 : OOB, 0,
-                                                  VASR_ROWS_STORE_AUX);
+    };
+    // n0 is wave-uniform: whole chunks branch (a per-lane select ran softplus's exp / log on
+    // every chunk and discarded it: 33.4 vs 39 us for the composed head GEMM, profiles/r03t)
+    if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
+        if (n0 >= p.n_out) body(std::integral_constant<int, 1>());
+        else if (n0 + 32 <= p.n_out) body(std::integral_constant<int, 0>());
+        else body(std::integral_constant<int, 2>());
+    } else {
+        body(std::integral_constant<int, 0>());
     }
 }
 
@@ -220,32 +229,20 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
     // C as a raw buffer over its valid bytes (the host checks they fit 31 bits)
     const int c_bytes = (EPI == VASR_EPI_ARGMAX ? 8 : 4) * ((p.M - 1) * (int)p.ldc + (EPI == VASR_EPI_ARGMAX ? NT : p.N));
     const __amdgpu_buffer_rsrc_t cbuf = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, c_bytes, 0x00020000);
-    // accumulators: two sets of SUPER chunk tiles; a set's SUPER epilogues run back to back (so a
-    // row's SUPER x 128 B of C go out together) while the other set accumulates
-    floatx16 acc[2][SUPER];
-    auto epi_group = [&](auto Sc, int g, int n) {  // the n <= SUPER tiles of group g from set S
+    // two accumulator sets: chunk j's MFMAs into set j & 1 while chunk j - 1's epilogue stores
+    // (set (j - 1) & 1) drain
+    floatx16 acc[2];
+    // chunk j into set S: wait for its DMA (counted: younger DMAs and stores stay in flight),
+    // publish it block-wide (the barrier also certifies every wave is done with the slot
+    // DMA(j + DEPTH) refills), chunk j - 1's epilogue, prefetch chunk j + DEPTH, chunk j's MFMAs
+    auto step = [&](auto Sc, int j) {
         constexpr int S = decltype(Sc)::value;
-#pragma unroll
-        for (int t = 0; t < SUPER; ++t)
-            if (t < n) rows_epilogue<EPI>(p, cbuf, m0, (c0 + g * SUPER + t) * 32, acc[S][t], r, h, bias_s, qp_s, cfirst);
-    };
-    // store instructions this wave issues at step k: the whole previous group's at a group's first step
-    auto stores_at = [&](int k) { return (k % SUPER == 0 && k >= SUPER) ? NST * SUPER : 0; };
-    // chunk j (tile T of group j / SUPER, set S): wait for its DMA (counted: younger DMAs and
-    // stores stay in flight), publish it block-wide (the barrier also certifies every wave is done
-    // with the slot DMA(j + DEPTH) refills), drain the previous group at a group's first chunk,
-    // prefetch chunk j + DEPTH, then chunk j's MFMAs
-    auto step = [&](auto Sc, auto Tc, int j) {
-        constexpr int S = decltype(Sc)::value;
-        constexpr int T = decltype(Tc)::value;
         // vector-memory ops this wave issued after DMA(j): the DMAs of chunks j + 1 .. j + DEPTH - 1
-        // and the epilogue stores of the steps after the one that issued DMA(j) (step j - DEPTH,
-        // or the prologue); older stores must have retired, younger ones stay in flight
+        // and the epilogue stores of steps j - DEPTH + 1 .. j - 1 (step k >= 1 stores chunk k - 1);
+        // older stores must have retired, younger ones stay in flight
         int n_vm = 0;
         if (loader && !((VASR_ROWS_ABLATE & 4) && j >= 1)) n_vm = (min(j + DEPTH - 1, nc - 1) - j) * NDMA;
-        if (!(VASR_ROWS_ABLATE & 2))
-            for (int k = max(j - DEPTH + (VASR_ROWS_ISSUE_FIRST ? 0 : 1), 0); k < j; ++k) n_vm += stores_at(k);
-        if (VASR_ROWS_NOSTWAIT && !loader) n_vm = 63;  // no DMA to wait for: stores stay in flight
+        if (!(VASR_ROWS_ABLATE & 2)) n_vm += NST * max(0, j - max(j - DEPTH + 1, 1));
         wait_vmcnt_rt(min(n_vm, 63));
         if (!(VASR_ROWS_ABLATE & 8)) __builtin_amdgcn_s_barrier();
         const char* wb = slot((VASR_ROWS_ABLATE & 4) ? min(j, DEPTH - 1) : j % NSLOT) + lane * 16;
@@ -253,9 +250,8 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         bf16x8 wf[2][3];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) wf[0][pl] = *reinterpret_cast<const bf16x8*>(wb + pl * 1024);
-        if (VASR_ROWS_ISSUE_FIRST && j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
-        if (T == 0 && j >= SUPER) epi_group(std::integral_constant<int, S ^ 1>(), j / SUPER - 1, SUPER);
-        if (!VASR_ROWS_ISSUE_FIRST && j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
+        if (j >= 1) rows_epilogue<EPI>(p, cbuf, m0, (c0 + j - 1) * 32, acc[S ^ 1], r, h, bias_s, qp_s, cfirst);
+        if (j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
         floatx16 c;
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = 0.f;
@@ -281,21 +277,14 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][0], wf[cur][0], c, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-        acc[S][T] = c;
+        acc[S] = c;
     };
-    auto group = [&](auto Sc, int j0) {  // the chunks of one group, tiles 0 .. SUPER-1
-        step(Sc, std::integral_constant<int, 0>(), j0);
-        if constexpr (SUPER > 1) if (j0 + 1 < nc) step(Sc, std::integral_constant<int, 1>(), j0 + 1);
-        if constexpr (SUPER > 2) if (j0 + 2 < nc) step(Sc, std::integral_constant<int, 2>(), j0 + 2);
-        if constexpr (SUPER > 3) if (j0 + 3 < nc) step(Sc, std::integral_constant<int, 3>(), j0 + 3);
-    };
-    for (int j = 0; j < nc; j += 2 * SUPER) {
-        group(std::integral_constant<int, 0>(), j);
-        if (j + SUPER < nc) group(std::integral_constant<int, 1>(), j + SUPER);
+    for (int j = 0; j < nc; j += 2) {
+        step(std::integral_constant<int, 0>(), j);
+        if (j + 1 < nc) step(std::integral_constant<int, 1>(), j + 1);
     }
-    const int gl = (nc - 1) / SUPER;  // the last group, drained here
-    if (gl & 1) epi_group(std::integral_constant<int, 1>(), gl, nc - gl * SUPER);
-    else epi_group(std::integral_constant<int, 0>(), gl, nc - gl * SUPER);
+    const int jl = nc - 1;  // the last chunk's epilogue
+    rows_epilogue<EPI>(p, cbuf, m0, (c0 + jl) * 32, (jl & 1) ? acc[1] : acc[0], r, h, bias_s, qp_s, cfirst);
 }
 
 template <int KS>
