@@ -133,16 +133,43 @@ struct HalfReduce {
     static __device__ __forceinline__ int step(int j, int g) { return j + SF * (g >> (LG - NSPLIT)); }
 };
 
-template <int CTRL, int S>
-__device__ __forceinline__ void butterfly_level(float (&v)[8], bool sel) {
+// One exchange of a level: lanes with sel = 0 get lo + partner's lo, lanes with sel = 1 get
+// hi + partner's hi (the partner has the other sel).  Where sel is a whole DPP row or bank of
+// the lane index, two bank-/row-masked DPP adds do it (each writes only its half of the lanes);
+// the lane ^ 16 exchange is one v_permlane16_swap (rows 1 / 3 of lo trade places with rows 0 / 2
+// of hi) and one add; other levels select with v_cndmask first (3 VALU instead of 2).  The
+// sums are the same pairs, so every variant gives the same bits.
+template <int CTRL, int SELBIT>
+__device__ __forceinline__ float exchange_add(float lo, float hi, bool sel) {
+    if constexpr (CTRL == -1) {
+        static_assert(SELBIT == 4, "lane ^ 16: sel = bit 4");
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    } else if constexpr ((CTRL == 0x140 && SELBIT == 3) || (CTRL == 0x141 && SELBIT == 2)) {
+        float s;
+        // banks (4-lane groups of a row) with sel = 0 / 1; s_nop 1: the VALU -> DPP read wait states
+        if constexpr (CTRL == 0x140)
+            asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+                         "v_add_f32_dpp %0, %2, %2 row_mirror row_mask:0xf bank_mask:0xc"
+                         : "=&v"(s) : "v"(lo), "v"(hi));
+        else
+            asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %1, %1 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
+                         "v_add_f32_dpp %0, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xa"
+                         : "=&v"(s) : "v"(lo), "v"(hi));
+        return s;
+    } else {
+        const float keep = sel ? hi : lo;
+        const float send = sel ? lo : hi;
+        return keep + xchg<CTRL>(send);
+    }
+}
+
+template <int CTRL, int S, int SELBIT = 0>
+__device__ __forceinline__ void butterfly_level(float (&v)[8], int g) {
     if constexpr (S >= 2) {
+        const bool sel = (g >> SELBIT) & 1;
 #pragma unroll
-        for (int j = 0; j < S / 2; ++j) {
-            const float lo = v[j], hi = v[j + S / 2];
-            const float keep = sel ? hi : lo;
-            const float send = sel ? lo : hi;
-            v[j] = keep + xchg<CTRL>(send);
-        }
+        for (int j = 0; j < S / 2; ++j) v[j] = exchange_add<CTRL, SELBIT>(v[j], v[j + S / 2], sel);
     } else {
         v[0] = v[0] + xchg<CTRL>(v[0]);
     }
@@ -151,24 +178,24 @@ __device__ __forceinline__ void butterfly_level(float (&v)[8], bool sel) {
 template <int G>
 __device__ __forceinline__ void reduce_half(float (&v)[8], int g) {
     if constexpr (G == 32) {
-        butterfly_level<-1, 8>(v, (g >> 4) & 1);     // ds_swizzle: lane ^ 16
-        butterfly_level<0x140, 4>(v, (g >> 3) & 1);  // row_mirror: lane ^ 15
-        butterfly_level<0x141, 2>(v, (g >> 2) & 1);  // row_half_mirror: lane ^ 7
-        butterfly_level<0x4E, 1>(v, false);          // quad_perm [2,3,0,1]: lane ^ 2
-        butterfly_level<0xB1, 1>(v, false);          // quad_perm [1,0,3,2]: lane ^ 1
+        butterfly_level<-1, 8, 4>(v, g);     // v_permlane16_swap: lane ^ 16
+        butterfly_level<0x140, 4, 3>(v, g);  // row_mirror: lane ^ 15
+        butterfly_level<0x141, 2, 2>(v, g);  // row_half_mirror: lane ^ 7
+        butterfly_level<0x4E, 1>(v, g);      // quad_perm [2,3,0,1]: lane ^ 2
+        butterfly_level<0xB1, 1>(v, g);      // quad_perm [1,0,3,2]: lane ^ 1
     } else if constexpr (G == 16) {
-        butterfly_level<0x140, 8>(v, (g >> 3) & 1);  // row_mirror: lane ^ 15
-        butterfly_level<0x141, 4>(v, (g >> 2) & 1);  // row_half_mirror: lane ^ 7
-        butterfly_level<0x4E, 2>(v, (g >> 1) & 1);   // quad_perm [2,3,0,1]: lane ^ 2
-        butterfly_level<0xB1, 1>(v, false);          // quad_perm [1,0,3,2]: lane ^ 1
+        butterfly_level<0x140, 8, 3>(v, g);  // row_mirror: lane ^ 15
+        butterfly_level<0x141, 4, 2>(v, g);  // row_half_mirror: lane ^ 7
+        butterfly_level<0x4E, 2, 1>(v, g);   // quad_perm [2,3,0,1]: lane ^ 2
+        butterfly_level<0xB1, 1>(v, g);      // quad_perm [1,0,3,2]: lane ^ 1
     } else if constexpr (G == 8) {
-        butterfly_level<0x141, 8>(v, (g >> 2) & 1);
-        butterfly_level<0x4E, 4>(v, (g >> 1) & 1);
-        butterfly_level<0xB1, 2>(v, g & 1);
+        butterfly_level<0x141, 8, 2>(v, g);
+        butterfly_level<0x4E, 4, 1>(v, g);
+        butterfly_level<0xB1, 2, 0>(v, g);
     } else {
         static_assert(G == 4, "G in {4, 8, 16, 32}");
-        butterfly_level<0x4E, 8>(v, (g >> 1) & 1);
-        butterfly_level<0xB1, 4>(v, g & 1);
+        butterfly_level<0x4E, 8, 1>(v, g);
+        butterfly_level<0xB1, 4, 0>(v, g);
     }
 }
 
