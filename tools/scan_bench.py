@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Micro-benchmark of vasr_ssm_scan_f32 alone at the C2 shape (B=32, L=501, Di=384, N=64)."""
+"""Micro-benchmark of vasr_ssm_scan_f32 alone at the C2 shape (B=32, L=501, Di=384, N=64): `reps`
+launches captured in one HIP graph and replayed (per-launch kernel time, no host cost)."""
 import os
 import sys
 import time
@@ -25,10 +26,18 @@ def main():
     for _ in range(5):
         ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode, out=out)
     torch.cuda.synchronize()
+    # the launches replayed from a HIP graph: kernel time without the host wrapper's per-call cost
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=st):
+        for _ in range(reps):
+            ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode, out=out)
+    gr.replay()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode, out=out)
+    gr.replay()
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / reps * 1e3
