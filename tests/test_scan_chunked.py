@@ -84,11 +84,14 @@ def test_chunked_state_dims_and_model_width(tc, N, Di):
 
 @pytest.mark.gpu
 def test_chunked_is_the_default_for_one_utterance():
-    """The model shape at B = 1 takes the chunked form; at the bench's 16-clip launches the
-    streaming kernel (enough waves)."""
+    """The model shape at B = 1 takes the chunked form; at the bench's 16-clip launches, at
+    B = 4 (384 waves) and for the global blocks' short L the streaming kernel (profiles/r03ae)."""
     from velocity_asr import ops
-    assert ops._use_chunked(1, 501, 384, 64, 2) and ops._use_chunked(4, 1501, 384, 64, 0)
+    assert ops._use_chunked(1, 501, 384, 64, 2) and ops._use_chunked(2, 1501, 384, 64, 0)
+    assert ops._use_chunked(1, 187, 384, 32, 2)
     assert not ops._use_chunked(16, 501, 384, 64, 2)
+    assert not ops._use_chunked(4, 501, 384, 64, 2)
+    assert not ops._use_chunked(1, 64, 384, 32, 2)   # the global blocks at 10 s
     assert not ops._use_chunked(1, 501, 384, 64, 1)  # the recurrence keeps its own kernel
     assert not ops._use_chunked(1, 16, 384, 64, 2)   # one chunk: nothing to parallelise
 

@@ -15,6 +15,8 @@ def main():
     B, L, Di, N = [int(v) for v in (sys.argv[1:5] if len(sys.argv) >= 5 else (32, 501, 384, 64))]
     mode = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     reps = int(sys.argv[6]) if len(sys.argv) > 6 else 50
+    if len(sys.argv) > 7:  # "streaming" | "chunked": force the form (default: by launch size)
+        ops.scan_form(sys.argv[7])
     g = torch.Generator(device="cuda").manual_seed(0)
     M = B * L
     xz = torch.randn(M, 2 * Di, device="cuda", generator=g)
@@ -42,7 +44,8 @@ def main():
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / reps * 1e3
     byts = B * L * (4 * Di + 2 * N) * 4
-    print(f"scan B={B} L={L} Di={Di} N={N} mode={mode}: {us:.1f} us/launch, {byts / us / 1e3:.1f} GB/s, "
+    form = sys.argv[7] if len(sys.argv) > 7 else "auto"
+    print(f"scan B={B} L={L} Di={Di} N={N} mode={mode} {form}: {us:.1f} us/launch, {byts / us / 1e3:.1f} GB/s, "
           f"{B * L * Di * N / us / 1e3:.1f} Gelem/s")
 
 

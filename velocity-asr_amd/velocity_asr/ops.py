@@ -400,10 +400,16 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
 
 
 # Chunk-parallel tree scan (vasr_ssm_scan_chunked_f32, bitwise equal to the streaming kernel)
-# for launches under CHUNKED_MAX_WAVES waves of the streaming kernel (B * Di * N / 256; 768 on
-# 1024 SIMDs): one utterance at a time, as the reference's scripts feed the model.
+# for launches under CHUNKED_MAX_WAVES waves of the streaming kernel (B * Di * N / 256 at 4 states
+# per lane) over more than CHUNKED_MIN_L steps: one utterance at a time, as the reference's
+# scripts feed the model.  Measured (profiles/r03ae/forms.txt, graph-timed): the streaming kernel
+# takes ~4.8 + 0.067 L us at these sizes whatever B; the chunked form's three launches win from
+# L ~ 150 while the launch is at most 192 waves (B = 1, 10 s: 14.7 vs 37.1 us at N = 32, 18.3 vs
+# 37.0 at N = 64) and lose at 384 (B = 4, N = 64: 41.9 vs 39.1) and for short L (the global
+# blocks' L = 64 at 10 s: 10.2 vs 6.8 us).
 # scan_form("streaming" | "chunked" | None) forces one (default from VASR_SCAN_CHUNKED=0|1).
-CHUNKED_MAX_WAVES = 512
+CHUNKED_MAX_WAVES = 256
+CHUNKED_MIN_L = 160
 _SCAN_FORM = {"0": "streaming", "1": "chunked"}.get(os.environ.get("VASR_SCAN_CHUNKED", ""))
 
 
@@ -422,7 +428,7 @@ def _use_chunked(B: int, Lq: int, Di: int, N: int, mode: int) -> bool:
         return False
     if _SCAN_FORM is not None:
         return _SCAN_FORM == "chunked"
-    return B * Di * N // 256 < CHUNKED_MAX_WAVES
+    return B * Di * N // 256 < CHUNKED_MAX_WAVES and Lq > CHUNKED_MIN_L
 
 
 SCAN_STATE_DIMS = (16, 32, 64, 128)  # the scan kernels' state dims (include/vasr.h)
