@@ -157,7 +157,7 @@ def kernel_roofline(model, audio, steps, streams=1):
         elems = i["B"] * i["L"] * i["Di"] * i["N"]
         t = float(np.mean([d for d, _ in scans]))
         out["scan"] = dict(t=t, bytes=bytes_per, elems=elems, launches=len(scans), per_step=len(scans) / steps,
-                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"], N=i["N"])
+                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"], N=i["N"], L=i["L"])
     g = rec["gemm"]
     flops = [2.0 * i["M"] * i["N"] * i["K"] * i["batch"] for _, i in g]
     groups = {}
@@ -462,8 +462,8 @@ def run(args):
         key = "gemm_x3"
     roof.update(gemm_fields)
     t = pmc_lookup("pmc_traffic.json", key)
-    if isinstance(t, dict) and sc and key == "ssm_scan":  # by launch grid: B x Di/16 blocks of 256 threads
-        t = t.get(str(sc["B"] * (sc["Di"] // 16) * 256))
+    if isinstance(t, dict) and sc and key == "ssm_scan":  # by launch grid (B x Di/16 x 256 threads) @ L
+        t = t.get("%d@%d" % (sc["B"] * (sc["Di"] // 16) * 256, sc["L"]))
     if isinstance(t, (int, float)):
         roof["traffic"] = t
     line = {

@@ -76,14 +76,18 @@ def main(tag):
                      f"{'' if wr is None else f'{wr / 1e6:.1f}'} |")
         fam = family(r["Name"])
         if fam in ("ssm_scan",) and rd is not None:
-            # grid size -> bytes, merged over the family's instantiations (chunk lengths, layouts)
-            traffic.setdefault(fam, {}).update({str(g): int(v[0] + v[1]) for _, g, v in cands})
+            # "grid size @ L" -> bytes, merged over the family's instantiations (chunk lengths,
+            # layouts); tools/profile.sh profiles the C2 bench, L = SCAN_L (501)
+            traffic.setdefault(fam, {}).update({f"{g}@{SCAN_L}": int(v[0] + v[1]) for _, g, v in cands})
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
-        json.dump(dict(run=tag, unit="bytes per launch (FETCH_SIZE*2 + WRITE_SIZE), by launch grid size (threads)", **traffic), f, indent=1)
+        json.dump(dict(run=tag, unit="bytes per launch (FETCH_SIZE*2 + WRITE_SIZE), by launch grid size (threads) "
+                                     "@ time steps", **traffic), f, indent=1)
     print("\n".join(lines[:14]))
 
+
+SCAN_L = int(os.environ.get("SCAN_L", "501"))  # time steps of the profiled bench's scans
 
 if __name__ == "__main__":
     main(sys.argv[1] if len(sys.argv) > 1 else "r01")
