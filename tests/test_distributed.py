@@ -1,4 +1,4 @@
-"""Multi-process plumbing of utterance sharding (gloo, world_size 2, CPU).
+"""Multi-process plumbing of utterance sharding (gloo, world_size 2 and 8, CPU).
 
 The HIP step is replaced by a CPU stand-in that reproduces the reference's greedy decode
 through the oracle on a deterministic fake "logit" function, so the test checks scatter
@@ -66,10 +66,11 @@ def _worker(rank, world, port, audio, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_transcription_matches_single_process(world):
+@pytest.mark.parametrize("world,clips", [(2, 6), (8, 16)])
+def test_sharded_transcription_matches_single_process(world, clips):
+    """world 8 rehearses C3's layout (an equal utterance shard per rank of one 8-GPU node)."""
     rng = np.random.default_rng(0)
-    audio = torch.from_numpy(rng.standard_normal((6, 3200)).astype(np.float32))
+    audio = torch.from_numpy(rng.standard_normal((clips, 3200)).astype(np.float32))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
