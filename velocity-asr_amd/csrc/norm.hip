@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
 #pragma unroll
                 for (int j = 0; j < KM; ++j) {
                     const int r = tt + j - (KM - 1);  // LN row tt + j of the tile
-                    acc += (r < 0 ? win[j + tt] : lv[r]) * w[j];
+                    acc = __builtin_fmaf(r < 0 ? win[j + tt] : lv[r], w[j], acc);  // one rounding per tap (every path)
                 }
                 yb[(int64_t)(t0 + tt) * C + c] = acc + bias;
             }
@@ -181,8 +181,8 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
             float acc = 0.f;
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
-                if (j < Kc - 1) acc += win[j] * w[j];
-                else if (j == Kc - 1) acc += v * w[j];
+                if (j < Kc - 1) acc = __builtin_fmaf(win[j], w[j], acc);
+                else if (j == Kc - 1) acc = __builtin_fmaf(v, w[j], acc);
             }
 #pragma unroll
             for (int j = 0; j + 1 < KM; ++j) {
