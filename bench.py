@@ -341,7 +341,10 @@ def run(args):
         Q.calibrate_from_activations(model, compute_mel_spectrogram(calib))
     S_len = int(args.seconds * SR)
     B = args.batch
-    streams = args.streams or (2 if B >= 8 else 1)
+    # one graph for the whole batch by default: two utterance groups replayed concurrently
+    # (--streams 2, 1.6 % faster on C2) gave group 1 wrong tokens in 0.5-8 % of replays
+    # (tools/diag/graph_stress.py; cause open); one graph: 0 of 400
+    streams = args.streams or 1
     audio = torch.from_numpy(S.make_audio(B, S_len, seed=1234 + rank)).to(dev)  # resident in HBM
 
     if args.eager:

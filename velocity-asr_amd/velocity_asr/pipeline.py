@@ -126,11 +126,6 @@ class GraphedTranscriber:
             with torch.cuda.graph(gr, stream=st):
                 audio_to_token_ids(model, v, out=o)
             self.graphs.append(gr)
-        # first replays one graph at a time, then a device sync: concurrent replays right after
-        # capture were the likeliest to give the second group wrong tokens
-        for gr in self.graphs:
-            gr.replay()
-            torch.cuda.synchronize(dev)
 
     def _check_params(self) -> None:
         if (list(map(_VERSION, self._tensors)) != self._versions
