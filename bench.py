@@ -199,7 +199,8 @@ def cpu_baseline():
     return dict(value=round(r["rtfx"], 3), unit="audio-sec/sec (RTFx)", cores=r["workers"], kind="port",
                 sample=f"the bench's 32 x 10 s clips (rank 0), one clip per call, mel+forward+greedy, "
                        f"oracle/velocity_ref.py with the reference's materialised tree scan (SCAN_FORM='tree'), "
-                       f"{r['workers']} single-thread worker processes (the job's CPU share; os.cpu_count()="
+                       f"{r['workers']} single-thread worker processes (BLAS threads per worker: "
+                       f"{r.get('blas_threads_per_worker')}; the job's CPU share; os.cpu_count()="
                        f"{os.cpu_count()}), median of 3 passes {r['passes_s']} s after a warm-up clip per worker; "
                        f"host CPU: {cpu_model()}; the real reference measured 7.95 RTFx on 8 Xeon threads in the "
                        f"build container (SURVEY §6)")
@@ -235,7 +236,7 @@ def _golden_lists(kind, rank, seconds, batch):
     except OSError:
         return None
     if seconds == 30.0 and kind == "fp32" and rank == 0:
-        ref = full["c4"]  # the first 8 clips of make_audio(32, 480000, seed=1234)
+        ref = full["c4"]  # all 32 clips of make_audio(32, 480000, seed=1234)
     elif seconds != 10.0:
         return None
     elif kind == "fp32":
@@ -368,18 +369,19 @@ def run(args):
         step()
     elapsed = timed(step, args.steps, world, dev)
 
-    # tokens of the timed graph vs an eager pass over the same audio, and vs the reference's
-    # greedy lists for the same clips (outside the timed region)
-    toks, lens = audio_to_token_ids(model, audio)
-    graph_match = True
-    if tr is not None:
-        from velocity_asr.pipeline import token_lists
-        gt, gl = tr.collect()
-        graph_match = token_lists(gt, gl) == token_lists(toks, lens)
-    gc = torch.tensor(golden_check(toks, lens, args, rank), device=dev, dtype=torch.float64)
+    # the tokens the timed graph wrote in its last replay vs the reference's greedy lists for the
+    # same clips, and an eager pass over the same audio checked the same way (outside the timed
+    # region)
+    from velocity_asr.pipeline import token_lists
+    etoks, elens = audio_to_token_ids(model, audio)
+    toks, lens = (t.clone() for t in tr.collect()) if tr is not None else (etoks, elens)
+    graph_match = token_lists(toks, lens) == token_lists(etoks, elens)
+    gc = torch.tensor(golden_check(toks, lens, args, rank) + golden_check(etoks, elens, args, rank),
+                      device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(gc)
-    golden = golden_summary([int(v) for v in gc.tolist()], args)
+    gc = [int(v) for v in gc.tolist()]
+    golden, golden_eager = golden_summary(gc[:7], args), golden_summary(gc[7:], args)
     valid = torch.arange(toks.shape[1], device=dev)[None, :] < lens[:, None]
     csum = torch.tensor([float(lens.sum().item()), float(toks.long().masked_fill(~valid, 0).sum().item())],
                         device=dev, dtype=torch.float64)
@@ -504,6 +506,7 @@ def run(args):
         "graph_tokens_match_eager": graph_match,
         "rank0_tokens_match_reference": None if golden is None else bool(golden["all_ranks_pass"]),
         "tokens_vs_reference": golden,
+        "eager_tokens_vs_reference": golden_eager,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()

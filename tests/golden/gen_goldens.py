@@ -483,6 +483,26 @@ def gen_fullbatch():
     save("fwd_fullbatch.npz", **out)
 
 
+def gen_c4full():
+    """All 32 clips of C4 = make_audio(32, 480000, seed=1234), written into
+    fwd_fullbatch.npz in place of the first-8 entries (c2 kept); the reference in chunks of 4.
+    The first 8 clips' greedy lists must equal the earlier chunks-of-2 run (batch invariance)."""
+    path = os.path.join(HERE, "fwd_fullbatch.npz")
+    old = np.load(path, allow_pickle=False)
+    out = {k: old[k] for k in old.files if k not in ("greedy", "meta")}
+    decoded = json.loads(str(old["greedy"]))
+    prev = decoded.get("c4")
+    model = build_model()
+    _tokens_pack("c4_", model, syn.make_audio(32, 480000, seed=1234), 4, out, decoded)
+    if prev is not None and decoded["c4"][:len(prev)] != prev:
+        raise AssertionError("C4: the first clips' reference tokens changed with the chunking")
+    out["greedy"] = np.array(json.dumps(decoded))
+    out["meta"] = meta(c2="make_audio(32, 160000, seed=1234), reference run in chunks of 8",
+                       c4="make_audio(32, 480000, seed=1234), all 32 clips, reference run in chunks of 4",
+                       weights="make_weights(None, seed=0)")
+    save("fwd_fullbatch.npz", **out)
+
+
 def _greedy_pack(prefix, model, audio, chunk, out, decoded, cast=None):
     """Like _tokens_pack for a model whose forward takes `cast(mel)` (bf16): argmax tokens and
     greedy lists only (margins are meaningless for the statistical configs)."""
@@ -614,6 +634,8 @@ if __name__ == "__main__":
         gen_beam()
     if "fullbatch" in which:
         gen_fullbatch()
+    if "c4full" in which:  # ~4 min on 8 threads: not in the default list
+        gen_c4full()
     if "benchsets" in which:  # long (~30 min on 8 threads): not in the default list
         gen_benchsets()
     if "statedims" in which:

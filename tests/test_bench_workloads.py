@@ -2,7 +2,7 @@
 
 bench.py rank r transcribes make_audio(32, 160000, seed=1234 + r) (C2 per rank, C3's 256 clips
 over 8 ranks); C5 is rank 0's batch through the INT8 fake-quant model.  Goldens:
-tests/golden/fwd_fullbatch.npz (rank 0 fp32, and C4's first 8 clips at 30 s) and
+tests/golden/fwd_fullbatch.npz (rank 0 fp32, and C4's 32 clips at 30 s) and
 tests/golden/fwd_benchsets.npz (ranks 1..7 fp32, ranks 0..7 bf16, rank 0 INT8), the reference
 CPU path run in chunks of 8 by tests/golden/gen_goldens.py::gen_benchsets.
 
@@ -83,9 +83,10 @@ def test_fp32_rank_batches_identical(va, fp32_model, sets, full, rank):
 
 
 def test_c4_30s_batch_identical(va, fp32_model, full):
-    """C4: the first 8 of the 32 x 30 s clips (the reference run in chunks of 2)."""
-    got = _lists(fp32_model, S.make_audio(8, 480000, seed=1234))
-    assert got == full["c4"]
+    """C4: all 32 x 30 s clips in one B = 32 launch (the reference run in chunks of 4)."""
+    got = _lists(fp32_model, S.make_audio(32, 480000, seed=1234))
+    bad = [i for i, (a, b) in enumerate(zip(got, full["c4"])) if a != b]
+    assert len(full["c4"]) == 32 and not bad, f"C4 clips {bad} differ from the reference"
 
 
 @pytest.mark.parametrize("rank", range(8))

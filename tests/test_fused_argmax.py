@@ -121,3 +121,8 @@ def test_graphed_transcriber_refuses_changed_weights(va):
         m.ctc_head.proj[2].bias.add_(1.0)
     with pytest.raises(RuntimeError, match="changed after capture"):
         gt.step()
+    # the replay that ran on the old weights is not handed out
+    with pytest.raises(RuntimeError, match="changed after capture"):
+        gt.collect()
+    torch.cuda.synchronize()
+    assert (gt.lengths == -1).all()

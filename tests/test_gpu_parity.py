@@ -289,7 +289,7 @@ def test_scan_gate_and_skip(va):
     ("short_400", lambda: S.make_audio(1, 400, seed=6)),
     ("oned_8000", lambda: S.make_audio(1, 8000, seed=9)[0]),
 ])
-@pytest.mark.parametrize("stft", ["fft", "fused", "gemm"])
+@pytest.mark.parametrize("stft", ["fft", "gemm"])
 def test_mel_matches_reference(va, name, make, stft, monkeypatch):
     from velocity_asr import audio as A
     monkeypatch.setattr(A, "_STFT_FFT", stft != "gemm")
@@ -326,16 +326,14 @@ def test_stft_power_fft_vs_fp64(va, S_):
 
 @pytest.mark.parametrize("S_", [160000, 201, 16333, 2559])
 def test_stft_power_fft_matches_dft_gemm(va, monkeypatch, S_):
-    """The fused FFT + log-mel launch equals the FFT launch + log-mel passes bit for bit (same
-    float operations), and both agree with the windowed-DFT GEMM (VASR_STFT=gemm) on the mel."""
+    """The real-FFT front end agrees with the windowed-DFT GEMM (VASR_STFT=gemm) on the mel."""
     from velocity_asr import audio as A
     x = t(S.make_audio(4, S_, seed=77))
     out = {}
-    for mode in ("fft", "fused", "gemm"):
+    for mode in ("fft", "gemm"):
         monkeypatch.setattr(A, "_STFT_FFT", mode != "gemm")
         monkeypatch.setattr(A, "_STFT_MODE", mode)
         out[mode] = A.mel_on_device(x).cpu()
-    assert torch.equal(out["fft"], out["fused"])
     np.testing.assert_allclose(out["fft"].numpy(), out["gemm"].numpy(), atol=2e-4, rtol=1e-4)
 
 
@@ -546,13 +544,18 @@ def test_full_batch_32x10s_properties(va, model):
 
 
 def test_full_batch_30s_pinned(va, model):
-    """BASELINE config 4 clips (make_audio(32, 480000, seed=1234)[:8], L = 1501): tokens and
-    greedy lists equal the reference's for all 8 pinned clips."""
-    audio = t(S.make_audio(32, 480000, seed=1234)[:8])
+    """BASELINE config 4 as the bench launches it (make_audio(32, 480000, seed=1234), one B = 32
+    forward, L = 1501): argmax tokens and greedy lists equal the reference's for all 32 clips
+    (tests/golden/fwd_fullbatch.npz, the reference run in chunks of 4), and the token pipeline
+    (fused CTC-head argmax + device collapse) gives the same lists."""
+    from velocity_asr.pipeline import audio_to_token_ids, token_lists
+    audio = t(S.make_audio(32, 480000, seed=1234))
     logits = model(va.compute_mel_spectrogram(audio))
     g = golden("fwd_fullbatch.npz")
     _assert_tokens_pinned(logits.argmax(-1).cpu().numpy(), va.ctc_greedy_decode(logits), g, "c4_",
-                          "C4 8 x 30 s")
+                          "C4 32 x 30 s")
+    del logits
+    assert token_lists(*audio_to_token_ids(model, audio)) == json.loads(str(g["greedy"]))["c4"]
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 64, 192), (33, 1280, 192), (501, 1280, 192), (8016, 1280, 192),

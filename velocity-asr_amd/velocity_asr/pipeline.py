@@ -87,6 +87,7 @@ class GraphedTranscriber:
     def __init__(self, model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
                  warmup: int = 2, streams: int = 1):
         self.model = model
+        self._stale = False
         dev = device or next(model.parameters()).device
         self.device = dev
         if batch % streams:
@@ -130,6 +131,10 @@ class GraphedTranscriber:
     def _check_params(self) -> None:
         if (list(map(_VERSION, self._tensors)) != self._versions
                 or [t.data_ptr() for t in self._tensors] != self._ptrs):
+            # the replay just issued ran on the old weights: mark its outputs invalid (lengths -1,
+            # ordered after the replay on the caller's stream) so collect() cannot hand them out
+            self._stale = True
+            self.lengths.fill_(-1)
             raise RuntimeError("GraphedTranscriber: the model's parameters changed after capture "
                                "(the graphs read the old weights); build a new GraphedTranscriber")
 
@@ -166,5 +171,9 @@ class GraphedTranscriber:
         self._check_params()
 
     def collect(self):
-        """(tokens, lengths) of the last step (the static outputs)."""
+        """(tokens, lengths) of the last step (the static outputs).  Raises once a step found
+        the parameters changed since capture (its outputs came from the old weights)."""
+        if self._stale:
+            raise RuntimeError("GraphedTranscriber: the last step ran on weights that changed after capture; "
+                               "build a new GraphedTranscriber")
         return self.tokens, self.lengths
