@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../velocity-asr_amd"
 OUT=../tools/_variants/$NAME; mkdir -p "$OUT"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -munsafe-fp-atomics $*"
 for f in csrc/*.hip csrc/*.cpp; do
-  extra=""; [ "$(basename $f)" = scan.hip ] && extra="-fno-slp-vectorize -ffp-contract=off"
+  extra=""; case "$(basename $f)" in scan*.hip) extra="-fno-slp-vectorize -ffp-contract=off";; esac
   /opt/rocm/bin/hipcc $FLAGS $extra -c "$f" -o "$OUT/$(basename $f).o" &
 done
 wait

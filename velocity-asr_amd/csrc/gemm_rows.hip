@@ -237,12 +237,15 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
     // DMA(j + DEPTH) refills), chunk j - 1's epilogue, prefetch chunk j + DEPTH, chunk j's MFMAs
     auto step = [&](auto Sc, int j) {
         constexpr int S = decltype(Sc)::value;
-        // vector-memory ops this wave issued after DMA(j): the DMAs of chunks j + 1 .. j + DEPTH - 1
-        // and the epilogue stores of steps j - DEPTH + 1 .. j - 1 (step k >= 1 stores chunk k - 1);
-        // older stores must have retired, younger ones stay in flight
+        // A loader wave waits for everything it issued: its DMA(j) has epilogue stores issued
+        // after it (step j - 1 stores chunk j - 2), and vmcnt counts loads and stores together
+        // with a store able to complete before an older load, so no count above 0 proves DMA(j)
+        // landed (the scan's fix of the same mistake: scan_body.inc, profiles/r04b/).  DMA(j + 1)
+        // and those stores were issued a whole chunk of MFMAs ago.  The other waves issue stores
+        // only (one event type: in order): they keep the stores of steps j - DEPTH + 1 .. j - 1 in
+        // flight and bound the older ones.
         int n_vm = 0;
-        if (loader && !((VASR_ROWS_ABLATE & 4) && j >= 1)) n_vm = (min(j + DEPTH - 1, nc - 1) - j) * NDMA;
-        if (!(VASR_ROWS_ABLATE & 2)) n_vm += NST * max(0, j - max(j - DEPTH + 1, 1));
+        if (!loader && !(VASR_ROWS_ABLATE & 2)) n_vm = NST * max(0, j - max(j - DEPTH + 1, 1));
         wait_vmcnt_rt(min(n_vm, 63));
         if (!(VASR_ROWS_ABLATE & 8)) __builtin_amdgcn_s_barrier();
         const char* wb = slot((VASR_ROWS_ABLATE & 4) ? min(j, DEPTH - 1) : j % NSLOT) + lane * 16;
