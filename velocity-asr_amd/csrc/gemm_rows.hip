@@ -34,16 +34,17 @@ using namespace gemm;
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
 // LDS-DMA of 16 B per lane into dst_base + 16 * lane (untracked by the compiler's waitcnt
 // model, ordered by the kernel: counted vmcnt + barrier; the memory clobber keeps the
 // epilogue's stores ahead of it in issue order)
 __device__ __forceinline__ void glds16(const void* src, void* dst_base) {
     const unsigned lds = (unsigned)(uintptr_t)(lds_void*)dst_base;
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+    // M0 is compiler-reserved: saved and restored inside the statement, and the SALU write of M0
+    // needs one wait state before the LDS-DMA reads it (s_nop 0)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds), "v"(src) : "memory");
 }
-#pragma clang diagnostic pop
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -66,6 +67,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 constexpr int RW = VASR_ROWS_WAVES;  // waves per block (4: one per SIMD)
 constexpr int DEPTH = VASR_ROWS_DEPTH;
 constexpr int NSLOT = DEPTH + 1;
+#ifndef VASR_ROWS_STORE_WAIT
+#define VASR_ROWS_STORE_WAIT 1  // 0: the store-only waves never wait for their older stores
+#endif
 #ifndef VASR_ROWS_MAX_GROUP
 #define VASR_ROWS_MAX_GROUP 16
 #endif
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         // only (one event type: in order): they keep the stores of steps j - DEPTH + 1 .. j - 1 in
         // flight and bound the older ones.
         int n_vm = 0;
-        if (!loader && !(VASR_ROWS_ABLATE & 2)) n_vm = NST * max(0, j - max(j - DEPTH + 1, 1));
+        if (!loader && !(VASR_ROWS_ABLATE & 2)) n_vm = VASR_ROWS_STORE_WAIT ? NST * max(0, j - max(j - DEPTH + 1, 1)) : 63;
         wait_vmcnt_rt(min(n_vm, 63));
         if (!(VASR_ROWS_ABLATE & 8)) __builtin_amdgcn_s_barrier();
         const char* wb = slot((VASR_ROWS_ABLATE & 4) ? min(j, DEPTH - 1) : j % NSLOT) + lane * 16;

@@ -54,13 +54,14 @@ __device__ __forceinline__ int a_swz(int r) { return ((r >> 1) & 3) ^ (((r >> 3)
 // tracking loses the slot distinction across the loop back edge and drains the ring).  The
 // kernel orders these loads itself: counted vmcnt + barrier before a slot is read.  Extra
 // untracked vector-memory operations can only make the compiler's own vmcnt waits stricter.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void glds16(const void* src, void* dst_base) {
     const unsigned lds = (unsigned)(uintptr_t)(lds_void*)dst_base;
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory", "m0");
+    // M0 is compiler-reserved: saved and restored inside the statement, and the SALU write of M0
+    // needs one wait state before the LDS-DMA reads it (s_nop 0)
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "s"(lds), "v"(src) : "memory");
 }
-#pragma clang diagnostic pop
 
 // vmcnt(n) with lgkmcnt / expcnt left open (gfx9 s_waitcnt encoding).
 template <int N>

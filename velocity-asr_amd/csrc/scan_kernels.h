@@ -56,18 +56,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 #ifndef VASR_SCAN_FASTSTAGE
 #define VASR_SCAN_FASTSTAGE 1  // 0: every chunk's staging addresses from the clamped index path
 #endif
-#ifndef VASR_SCAN_PREPASS_SYNC
-#define VASR_SCAN_PREPASS_SYNC 0  // diagnostic builds: 1 = block barrier after the {dt, x*dt} pre-pass
-#endif
-#ifndef VASR_SCAN_TREE_FMA
-#define VASR_SCAN_TREE_FMA 1  // diagnostic builds: 0 = mode 2's tree as multiply + add
-#endif
-#ifndef VASR_SCAN_PREPASS
-#define VASR_SCAN_PREPASS 1  // diagnostic builds: 0 = mode 2 forms x * dt per lane (no pre-pass slab)
-#endif
-#ifndef VASR_SCAN_PACKED_Y
-#define VASR_SCAN_PACKED_Y 1  // diagnostic builds: 0 = the 4-per-lane y partial as scalar fmas
-#endif
 #ifndef VASR_SCAN_PACKED
 #define VASR_SCAN_PACKED 1  // 1: state pairs as float2 vectors (v_pk_*_f32); 0: scalar pairs
 #endif
@@ -151,16 +139,9 @@ struct HalfReduce {
 // the lane ^ 16 exchange is one v_permlane16_swap (rows 1 / 3 of lo trade places with rows 0 / 2
 // of hi) and one add; other levels select with v_cndmask first (3 VALU instead of 2).  The
 // sums are the same pairs, so every variant gives the same bits.
-#ifndef VASR_SCAN_XCHG_GENERIC
-#define VASR_SCAN_XCHG_GENERIC 0  // diagnostic builds: 1 = every exchange as select + dpp_mov / ds_swizzle
-#endif
 template <int CTRL, int SELBIT>
 __device__ __forceinline__ float exchange_add(float lo, float hi, bool sel) {
-    if constexpr (VASR_SCAN_XCHG_GENERIC) {
-        const float keep = sel ? hi : lo;
-        const float send = sel ? lo : hi;
-        return keep + xchg<CTRL>(send);
-    } else if constexpr (CTRL == -1) {
+    if constexpr (CTRL == -1) {
         static_assert(SELBIT == 4, "lane ^ 16: sel = bit 4");
         const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
         return __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -235,7 +216,7 @@ __device__ __forceinline__ void flush_half(float (&yv)[TC], float* yp, int dl, i
 template <bool FMA>
 __device__ __forceinline__ f2 mad2(f2 a, f2 b, f2 c) {
 #pragma clang fp contract(off)
-    if constexpr (FMA && VASR_SCAN_TREE_FMA) {
+    if constexpr (FMA) {
 #if VASR_SCAN_PACKED
         return __builtin_elementwise_fma(a, b, c);
 #else
