@@ -38,7 +38,7 @@ def test_two_group_graphs_every_replay_matches_reference(model):
     ref = json.loads(str(golden("fwd_fullbatch.npz")["greedy"]))["c2"]
     audio = torch.from_numpy(S.make_audio(32, 160000, seed=1234)).to(DEV)
     tr = GraphedTranscriber(model, 32, 160000, streams=2)
-    assert not tr.serial and len(tr.graphs) == 2
+    assert len(tr.graphs) == 2
     bad = []
     for r in range(12):
         tr.audio.zero_()
@@ -51,6 +51,23 @@ def test_two_group_graphs_every_replay_matches_reference(model):
 
 def _bits(t):
     return t.contiguous().view(torch.int32)
+
+
+def test_two_one_clip_groups_match_eager(model):
+    """Two utterance groups of ONE clip each (the world-1 layout of test_distributed_gpu.py; the
+    chunk-parallel scan runs at B = 1) replayed concurrently 40 times: tokens equal eager's."""
+    from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids, token_lists
+    audio = torch.from_numpy(S.make_audio(2, 160000, seed=1234)).to(DEV)
+    with torch.no_grad():
+        exp = token_lists(*audio_to_token_ids(model, audio))
+    tr = GraphedTranscriber(model, 2, 160000, streams=2)
+    tr.audio.copy_(audio)
+    bad = []
+    for r in range(40):
+        tr.step()
+        got = token_lists(*tr.collect())
+        bad += [(r, i) for i in range(2) if got[i] != exp[i]]
+    assert not bad, f"(replay, clip) with tokens different from eager: {bad[:12]}"
 
 
 def test_scan_beside_coresident_gemms_is_bitwise_alone(model):

@@ -89,6 +89,23 @@ def first_diff(probes, refs):
         if bool(d.any()):
             flat = d.reshape(d.shape[0], -1).any(1).nonzero().flatten()
             rows = flat.tolist()
+            if os.environ.get("DETAIL"):
+                idx = d.reshape(-1).nonzero().flatten()
+                got_v = t.contiguous().reshape(-1)[idx[:12]].tolist()
+                ref_v = r.view(torch.float32).reshape(-1)[idx[:12]].tolist() if t.dtype == torch.float32 else []
+                runs = (idx[1:] - idx[:-1] != 1).sum().item() + 1
+                print(f"   {n}: flat {idx[:12].tolist()} .. {idx[-1].item()} ({runs} runs); got {got_v}; ref {ref_v}; "
+                      f"base {t.data_ptr():#x}", flush=True)
+                # where else does each wrong value occur bitwise in the references (either group)?
+                pos = [i for i, (pn, _) in enumerate(probes) if pn == n][0]
+                for e in idx[:4].tolist():
+                    gv = b.reshape(-1)[e]
+                    hits = []
+                    for gg in range(2):
+                        rr = ref[gg][pos][1].reshape(-1)
+                        w = (rr == gv).nonzero().flatten()[:4].tolist()
+                        hits += [(gg, x) for x in w]
+                    print(f"     elem {e}: got bits found at (group, flat) {hits}", flush=True)
             return n, int(d.sum()), (rows[0], rows[-1], len(rows), tuple(t.shape))
     return None
 
@@ -124,6 +141,11 @@ for b in range(BUILDS):
                 lo = min(t.data_ptr() for _, t in probes[g])
                 hi = max(t.data_ptr() + t.untyped_storage().nbytes() for _, t in probes[g])
                 print(f"group {g} probe span {lo:#x}..{hi:#x}", flush=True)
+            if os.environ.get("DETAIL"):  # every probe's extent, both groups, sorted by address
+                ext = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size(), g, n)
+                             for g in range(2) for n, t in probes[g])
+                for a0, a1, g, n in ext:
+                    print(f"   extent {a0:#x}..{a1:#x} g{g} {n}", flush=True)
     for r in range(REPS):
         if mode == "graph":
             streams[1].wait_stream(main)

@@ -54,20 +54,33 @@ __device__ __forceinline__ int a_swz(int r) { return ((r >> 1) & 3) ^ (((r >> 3)
 // tracking loses the slot distinction across the loop back edge and drains the ring).  The
 // kernel orders these loads itself: counted vmcnt + barrier before a slot is read.  Extra
 // untracked vector-memory operations can only make the compiler's own vmcnt waits stricter.
+#ifndef VASR_X3_STAGE
+#define VASR_X3_STAGE 0  // diagnostic builds only: 1 compiler LDS-DMA builtin, 2 register staging
+#endif
 __device__ __forceinline__ void glds16(const void* src, void* dst_base) {
+    if constexpr (VASR_X3_STAGE == 1) {
+        __builtin_amdgcn_global_load_lds(src, (lds_void*)dst_base, 16, 0, 0);
+    } else if constexpr (VASR_X3_STAGE == 2) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        reinterpret_cast<float4*>(dst_base)[threadIdx.x & 63] = v;
+    } else {
     const unsigned lds = (unsigned)(uintptr_t)(lds_void*)dst_base;
     // M0 is compiler-reserved: saved and restored inside the statement, and the SALU write of M0
     // needs one wait state before the LDS-DMA reads it (s_nop 0)
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "s"(lds), "v"(src) : "memory");
+    }
 }
 
 // vmcnt(n) with lgkmcnt / expcnt left open (gfx9 s_waitcnt encoding).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     static_assert(N >= 0 && N < 64, "vmcnt range");
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    if constexpr (VASR_X3_STAGE == 2)
+        __builtin_amdgcn_s_waitcnt(0);  // register staging: its LDS writes, before the barrier
+    else
+        __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 // P = 3: the split-bf16 fp32 GEMM described above.  P = 1: the bf16 GEMM of a bf16 model
@@ -298,7 +311,13 @@ __global__ __launch_bounds__(256, (x3_occ<WM, WN, TM, TN, RING, P>())) void gemm
             step(std::integral_constant<int, 3>(), kt + 3);
         }
     }
-    __syncthreads();  // LDS no longer read (the epilogue does not use it); drain for safety
+    // Drain this wave's LDS-DMA (the last step re-loads a stage nothing reads) before the epilogue
+    // may reuse the staging LDS and before the workgroup exits: the DMA is inline asm, untracked by
+    // the compiler, so __syncthreads() alone would not wait for it.  (Not the cause of the r04
+    // concurrent-stream STFT perturbation -- that one stays with register staging, profiles/r04l;
+    // see the Makefile's stft.hip rule.)
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+    __syncthreads();
 
     if constexpr (VASR_X3_ABLATE & 2) {  // keep every accumulator live, store nothing
         float sum = 0.f;

@@ -62,7 +62,6 @@ def _model_tensors(model: torch.nn.Module):
 
 
 _VERSION = operator.attrgetter("_version")
-SERIAL_MAX_GROUP = 2  # GraphedTranscriber: groups this small replay chained, not concurrently
 
 
 class GraphedTranscriber:
@@ -76,7 +75,11 @@ class GraphedTranscriber:
     writes its rows of the shared
     outputs.  The groups are independent (no padding masks, per-utterance statistics), so
     results are bitwise those of one graph, while the VALU-bound scan of one group overlaps
-    the MFMA-bound GEMMs of another on the same CUs (separate pipes).
+    the MFMA-bound GEMMs of another on the same CUs (separate pipes).  (Up to round 3 two groups
+    replayed concurrently could return wrong tokens for group 1: kernels of one stream disturbed
+    co-resident workgroups of the other: a scan LDS slab read back wrong, and the |STFT|^2 kernel's
+    packed-fp32 complex arithmetic came back wrong in one half-wave beside tile GEMMs.  Both code
+    forms are gone from the kernels; profiles/r04b-r04o.)
 
     The graphs are tied to the model's parameters as they were at capture: ``step()`` raises
     if any parameter or buffer was replaced or modified in place since (build a new
@@ -98,11 +101,6 @@ class GraphedTranscriber:
         self.tokens = torch.zeros((batch, L), device=dev, dtype=torch.int32)
         self.lengths = torch.zeros((batch,), device=dev, dtype=torch.int32)
         g = batch // streams
-        # groups of at most SERIAL_MAX_GROUP clips replay one after another: two such graphs
-        # replayed concurrently gave the second group wrong tokens in ~1 of 100-200 replays
-        # (tools/diag/graph_stress.py, 2 clips in 2 groups: 1/200 and 4/400 concurrent, 0/400
-        # chained or alone) -- cause not located, chained replay avoids it
-        self.serial = streams > 1 and g <= SERIAL_MAX_GROUP
         self.streams = [torch.cuda.Stream(dev) for _ in range(streams)]
         views = [self.audio[i * g:(i + 1) * g] for i in range(streams)]
         outs = [(self.tokens[i * g:(i + 1) * g], self.lengths[i * g:(i + 1) * g]) for i in range(streams)]
@@ -145,17 +143,6 @@ class GraphedTranscriber:
         tensors) overlaps the replay instead of delaying it.  The graphs only ever read storage
         this object keeps alive, so a failed check raises after a replay on the old weights."""
         main = torch.cuda.current_stream(self.device)
-        if self.serial:
-            self.graphs[0].replay()
-            prev = main
-            for st, gr in zip(self.streams[1:], self.graphs[1:]):
-                st.wait_stream(prev)
-                with torch.cuda.stream(st):
-                    gr.replay()
-                prev = st
-            main.wait_stream(prev)
-            self._check_params()
-            return
         # group 0 replays on the caller's stream itself: ordered with the caller's work without
         # cross-stream events (each event wait costs the device a queue-to-queue hop: one 10-s
         # utterance 0.602 vs 0.714 ms per step, C2 +1.3 %; profiles/r03ah/); the other groups on
