@@ -452,7 +452,7 @@ def run(args):
         tr.audio.copy_(audio)
 
     rf = kernel_roofline(model, audio, args.roofline_steps, 1 if args.eager else streams)
-    iso = isolated_times(model, audio)
+    iso = isolated_times(model, audio[:B // (1 if args.eager else streams)])  # one utterance group's launch shape
     if world > 1:
         dist.barrier()
     if rank != 0:
