@@ -79,12 +79,48 @@ def main(tag):
             # "grid size @ L" -> bytes, merged over the family's instantiations (chunk lengths,
             # layouts); tools/profile.sh profiles the C2 bench, L = SCAN_L (501)
             traffic.setdefault(fam, {}).update({f"{g}@{SCAN_L}": int(v[0] + v[1]) for _, g, v in cands})
+    lines += isolated_runs(os.path.join(src, "trace", "run_kernel_trace.csv"),
+                           os.path.join(src, "bench_trace.json"))
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
         json.dump(dict(run=tag, unit="bytes per launch (FETCH_SIZE*2 + WRITE_SIZE), by launch grid size (threads) "
                                      "@ time steps", **traffic), f, indent=1)
     print("\n".join(lines[:14]))
+
+
+def isolated_runs(trace, bench_json, reps=20):
+    """bench.py's isolated_times(): `reps` back-to-back launches of one kernel (after 3 warm-up
+    launches), timed by one HIP event pair.  Found in the kernel trace as runs of >= reps + 3
+    consecutive dispatches of one kernel; the last `reps` give the average kernel duration and
+    the span / reps (the event pair's quantity: durations plus dispatch gaps), to set beside the
+    avg_launch_us the profiled bench line printed."""
+    if not os.path.exists(trace):
+        return []
+    ks = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    runs, i = [], 0
+    while i < len(ks):
+        j = i
+        while j + 1 < len(ks) and ks[j + 1]["Kernel_Name"] == ks[i]["Kernel_Name"]:
+            j += 1
+        if j - i + 1 >= reps + 3:
+            sel = ks[j + 1 - reps:j + 1]
+            dur = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in sel) / reps / 1e3
+            span = (int(sel[-1]["End_Timestamp"]) - int(sel[0]["Start_Timestamp"])) / reps / 1e3
+            runs.append((short(ks[i]["Kernel_Name"]), j - i + 1, dur, span))
+        i = j + 1
+    out = ["", f"## Isolated back-to-back runs (bench.py isolated_times: 3 warm-up + {reps} timed launches)", "",
+           "| kernel | run length | avg kernel us (last 20) | span / 20 us |", "|---|---|---|---|"]
+    out += [f"| `{n[:70]}` | {ln} | {d:.2f} | {sp:.2f} |" for n, ln, d, sp in runs]
+    if os.path.exists(bench_json):
+        try:
+            r = json.load(open(bench_json))["roofline"]
+            out += ["", f"The profiled bench line (bench_trace.json, same process): avg_launch_us {r['avg_launch_us']} "
+                        f"({r['kernel'].split(' (')[0]}), gemm_avg_launch_us {r['gemm_avg_launch_us']} "
+                        f"({r['gemm_kernel']})."]
+        except (ValueError, KeyError):
+            pass
+    return out
 
 
 SCAN_L = int(os.environ.get("SCAN_L", "501"))  # time steps of the profiled bench's scans
