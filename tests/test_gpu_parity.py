@@ -558,7 +558,7 @@ def test_full_batch_30s_pinned(va, model):
     assert token_lists(*audio_to_token_ids(model, audio)) == json.loads(str(g["greedy"]))["c4"]
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 64, 192), (33, 1280, 192), (501, 1280, 192), (8016, 1280, 192),
+@pytest.mark.parametrize("M,N,K", [(1, 64, 192), (33, 1280, 192), (501, 1280, 192), (8016, 1280, 192), (16032, 1280, 192),
                                    (300, 1000, 192), (129, 96, 128), (77, 200, 100), (1024, 192, 192)])
 @pytest.mark.parametrize("epi", ["none", "gelu", "softplus", "residual", "argmax"])
 def test_gemm_rows_engine_bitwise_equals_tiles(va, M, N, K, epi):
