@@ -411,6 +411,10 @@ def run(args):
     etoks, elens = audio_to_token_ids(model, audio)
     toks, lens = (t.clone() for t in tr.collect()) if tr is not None else (etoks, elens)
     graph_match = token_lists(toks, lens) == token_lists(etoks, elens)
+    if world > 1:  # every rank's graph tokens against its eager pass
+        bad = torch.tensor([0.0 if graph_match else 1.0], device=dev, dtype=torch.float64)
+        dist.all_reduce(bad)
+        graph_match = bad.item() == 0
     gc = torch.tensor(golden_check(toks, lens, args, rank) + golden_check(etoks, elens, args, rank),
                       device=dev, dtype=torch.float64)
     if world > 1:
@@ -458,7 +462,7 @@ def run(args):
     if rank != 0:
         if distributed:
             dist.destroy_process_group()
-        return
+        return 0 if graph_match else 1
 
     audio_sec = world * B * args.seconds * args.steps
     frames = world * B * (S_len // 160 + 1) * args.steps
@@ -558,6 +562,11 @@ def run(args):
     print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
+    if not graph_match:  # the timed graphs' tokens differ from an eager pass: the line is not valid
+        log("bench.py: the timed graphs' tokens differ from an eager pass over the same audio "
+            "(graph_tokens_match_eager false); failing the run")
+        return 1
+    return 0
 
 
 def main():
@@ -567,7 +576,7 @@ def main():
     if args.inproc and args.gpus != 1:
         log("bench.py: --inproc runs one rank; use --gpus 1")
         sys.exit(2)
-    run(args)
+    sys.exit(run(args))
 
 
 if __name__ == "__main__":
