@@ -72,7 +72,8 @@ def parse_args(argv=None):
     ap.add_argument("--streams", type=int, default=0,
                     help="utterance groups replayed as separate HIP graphs on concurrent streams (the scan of one "
                          "group overlaps the GEMMs of the other; results are bitwise those of one graph); "
-                         "0 = 2 when the batch is an even number of at least 8 clips, else 1")
+                         "0 = build 1 and (for an even batch of at least 8 clips) 2, keep the faster "
+                         "(pipeline.autotuned_transcriber)")
     ap.add_argument("--int8", action="store_true",
                     help="BASELINE configs[4]: INT8 fake-quant model (prepare_model_for_qat + activation calibration)")
     ap.add_argument("--bf16", action="store_true",
@@ -376,11 +377,14 @@ def run(args):
         Q.calibrate_from_activations(model, compute_mel_spectrogram(calib))
     S_len = int(args.seconds * SR)
     B = args.batch
-    # two utterance groups on concurrent streams by default (the scan of one overlaps the GEMMs
-    # of the other).  Up to round 3 that raced (group 1 wrong tokens in 0.5-8 % of replays); the
-    # causes were in the kernels and are fixed, and every run checks the tokens the
-    # timed graphs wrote against the reference (tokens_vs_reference)
-    streams = args.streams or (2 if B >= 8 and B % 2 == 0 else 1)
+    # schedule: one graph of the batch or two utterance groups on concurrent streams (the scan of
+    # one overlaps the GEMMs of the other); bitwise the same tokens, and which is faster depends on
+    # the box, so by default both are built and the faster one (timed in the untimed warm-up) is
+    # kept (pipeline.autotuned_transcriber).  Up to round 3 the two-group form raced; the causes
+    # were in the kernels and are fixed, and every run checks the tokens the timed
+    # graphs wrote against the reference (tokens_vs_reference) and against an eager pass
+    streams = args.streams or 0
+    schedule = None
     audio = torch.from_numpy(S.make_audio(B, S_len, seed=1234 + rank)).to(dev)  # resident in HBM
 
     if args.eager:
@@ -388,7 +392,15 @@ def run(args):
             return audio_to_token_ids(model, audio)
         tr = None
     else:
-        tr = GraphedTranscriber(model, B, S_len, dev, streams=streams)
+        if streams:
+            tr = GraphedTranscriber(model, B, S_len, dev, streams=streams)
+        else:
+            from velocity_asr.pipeline import autotuned_transcriber
+            tr, tried = autotuned_transcriber(model, B, S_len, dev)
+            streams = len(tr.graphs)
+            schedule = dict(chosen_streams=streams, ms_per_replay_by_streams=tried,
+                            how="both schedules built and timed in the untimed warm-up (5 replays x 2 rounds each); "
+                                "the faster kept")
         tr.audio.copy_(audio)
         step = tr.step
 
@@ -537,7 +549,7 @@ def run(args):
                                f"(BASELINE configs[{4 if args.int8 else 2 if args.bf16 else 1}]"
                                f"{', INT8 fake-quant' if args.int8 else ''}"
                                f"{f', HIP graph x{streams} streams' if not args.eager else ', eager'})",
-                   "global_batch": world * B, "clip_seconds": args.seconds,
+                   "global_batch": world * B, "clip_seconds": args.seconds, "schedule": schedule,
                    "parallelism": f"utterance-shard x{world} over RCCL ({'resident shards; serving leg scatters from rank 0 and gathers tokens' if scatter else 'resident shards'})"
                    if distributed else "single process"},
         "frames_per_sec": round(frames / elapsed, 1),

@@ -104,3 +104,18 @@ def test_scan_beside_coresident_gemms_is_bitwise_alone(model):
         torch.cuda.synchronize()
     bad = [i for i, o in enumerate(outs) if not torch.equal(_bits(o), ref)]
     assert not bad, f"scan launches {bad} differ from the scan alone"
+
+
+def test_autotuned_schedule_matches_eager(model):
+    """pipeline.autotuned_transcriber builds one graph and two concurrent group graphs for 8 clips,
+    keeps the faster: its tokens equal eager's, and the timings it reports cover both."""
+    from velocity_asr.pipeline import audio_to_token_ids, autotuned_transcriber, token_lists
+    audio = torch.from_numpy(S.make_audio(8, 48000, seed=77)).to(DEV)
+    with torch.no_grad():
+        exp = token_lists(*audio_to_token_ids(model, audio))
+    tr, tried = autotuned_transcriber(model, 8, 48000, reps=2, rounds=1)
+    assert sorted(tried) == [1, 2] and len(tr.graphs) in (1, 2)
+    tr.audio.copy_(audio)
+    for _ in range(3):
+        tr.step()
+        assert token_lists(*tr.collect()) == exp

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import operator
 import os
+import time
 from typing import List, Optional, Tuple
 
 import torch
@@ -164,3 +165,43 @@ class GraphedTranscriber:
             raise RuntimeError("GraphedTranscriber: the last step ran on weights that changed after capture; "
                                "build a new GraphedTranscriber")
         return self.tokens, self.lengths
+
+
+def schedule_candidates(batch: int) -> List[int]:
+    """Stream counts GraphedTranscriber can use for `batch` clips: one graph of the whole batch,
+    and two utterance groups when the batch splits into groups of at least 4 clips."""
+    return [1, 2] if batch >= 8 and batch % 2 == 0 else [1]
+
+
+def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
+                          candidates: Optional[List[int]] = None, reps: int = 5, rounds: int = 2):
+    """The GraphedTranscriber schedule that runs fastest on this device.
+
+    One graph of the whole batch and two utterance-group graphs on concurrent streams give
+    bitwise the same tokens; which is faster depends on the box (round 4, C2 on two MI355X
+    boxes: 143.4k vs 140.4k RTFx for two groups on one, 146k vs 150k for one graph on another,
+    profiles/r04r, r04t).  Each candidate is built, replayed `reps` times per round after two
+    warm replays, rounds interleaved; the one with the lowest per-replay time is kept and the
+    others are released.  Returns (transcriber, {streams: best ms per replay}).  The
+    transcriber's audio holds zeros: copy the batch in before stepping."""
+    cands = list(candidates or schedule_candidates(batch))
+    trs = {s: GraphedTranscriber(model, batch, samples, device, streams=s) for s in cands}
+    if len(cands) == 1:
+        return trs[cands[0]], {}
+    times = {s: float("inf") for s in cands}
+    for _ in range(rounds):
+        for s, tr in trs.items():
+            tr.step()
+            tr.step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                tr.step()
+            torch.cuda.synchronize()
+            times[s] = min(times[s], (time.perf_counter() - t0) / reps * 1e3)
+    best = min(cands, key=lambda s: times[s])
+    keep = trs.pop(best)
+    del trs  # the other graphs and their memory pools
+    torch.cuda.synchronize()
+    return keep, {s: round(t, 4) for s, t in times.items()}
+
