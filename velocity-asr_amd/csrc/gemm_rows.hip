@@ -87,6 +87,15 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
     }
 }
 
+#ifdef VASR_ROWS_STAMPS
+// Diagnostic builds only: per-wave sums of the cycles (s_memtime) spent in each phase of a chunk
+// step, written once at the end of the kernel (no stores inside the loop), tools/diag/rows_stamps.py.
+__device__ unsigned long long* g_rows_stamps;
+#define VASR_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define VASR_STAMP(v)
+#endif
+
 // Epilogue of one 32 x 32 chunk held as one MFMA accumulator (the tile kernel's epilogue_body
 // arithmetic for TM = TN = 1), with the per-column bias / fake-quant parameters read from LDS
 // and the results written by raw buffer stores: exactly NST store instructions per wave and
@@ -236,6 +245,10 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
     // two accumulator sets: chunk j's MFMAs into set j & 1 while chunk j - 1's epilogue stores
     // (set (j - 1) & 1) drain
     floatx16 acc[2];
+#ifdef VASR_ROWS_STAMPS
+    unsigned long long st_wait = 0, st_bar = 0, st_epi = 0, st_dma = 0, st_mfma = 0;
+    VASR_STAMP(st_begin);
+#endif
     // chunk j into set S: wait for its DMA (counted: younger DMAs and stores stay in flight),
     // publish it block-wide (the barrier also certifies every wave is done with the slot
     // DMA(j + DEPTH) refills), chunk j - 1's epilogue, prefetch chunk j + DEPTH, chunk j's MFMAs
@@ -243,22 +256,29 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         constexpr int S = decltype(Sc)::value;
         // A loader wave waits for everything it issued: its DMA(j) has epilogue stores issued
         // after it (step j - 1 stores chunk j - 2), and vmcnt counts loads and stores together
-        // with a store able to complete before an older load, so no count above 0 proves DMA(j)
-        // landed (the scan's fix of the same mistake: scan_body.inc, profiles/r04b/).  DMA(j + 1)
-        // and those stores were issued a whole chunk of MFMAs ago.  The other waves issue stores
-        // only (one event type: in order): they keep the stores of steps j - DEPTH + 1 .. j - 1 in
+        // with a store able to complete before an older load, so a count that includes those
+        // stores does not prove DMA(j) landed (the scan's fix of the same mistake:
+        // scan_body.inc, profiles/r04b/).  (Counting only the younger DMA loads -- safe if loads
+        // retire in order among themselves -- measured no faster, 69.5 vs 68.7-70.5 us at
+        // M = 16032, profiles/r04v/, so the plain form stays.)  The other waves issue stores only
+        // (one event type: in order): they keep the stores of steps j - DEPTH + 1 .. j - 1 in
         // flight and bound the older ones.
         int n_vm = 0;
         if (!loader && !(VASR_ROWS_ABLATE & 2)) n_vm = VASR_ROWS_STORE_WAIT ? NST * max(0, j - max(j - DEPTH + 1, 1)) : 63;
+        VASR_STAMP(t0);
         wait_vmcnt_rt(min(n_vm, 63));
+        VASR_STAMP(t1);
         if (!(VASR_ROWS_ABLATE & 8)) __builtin_amdgcn_s_barrier();
+        VASR_STAMP(t2);
         const char* wb = slot((VASR_ROWS_ABLATE & 4) ? min(j, DEPTH - 1) : j % NSLOT) + lane * 16;
         // W fragments of k-step 0 first, so the chunk's first MFMA does not wait behind the epilogue
         bf16x8 wf[2][3];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) wf[0][pl] = *reinterpret_cast<const bf16x8*>(wb + pl * 1024);
         if (j >= 1) rows_epilogue<EPI>(p, cbuf, m0, (c0 + j - 1) * 32, acc[S ^ 1], r, h, bias_s, qp_s, cfirst);
+        VASR_STAMP(t3);
         if (j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
+        VASR_STAMP(t4);
         floatx16 c;
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = 0.f;
@@ -285,6 +305,14 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
             __builtin_amdgcn_sched_barrier(0);
         }
         acc[S] = c;
+#ifdef VASR_ROWS_STAMPS
+        VASR_STAMP(t5);
+        st_wait += t1 - t0;
+        st_bar += t2 - t1;
+        st_epi += t3 - t2;
+        st_dma += t4 - t3;
+        st_mfma += t5 - t4;
+#endif
     };
     for (int j = 0; j < nc; j += 2) {
         step(std::integral_constant<int, 0>(), j);
@@ -292,6 +320,15 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
     }
     const int jl = nc - 1;  // the last chunk's epilogue
     rows_epilogue<EPI>(p, cbuf, m0, (c0 + jl) * 32, (jl & 1) ? acc[1] : acc[0], r, h, bias_s, qp_s, cfirst);
+#ifdef VASR_ROWS_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    VASR_STAMP(st_end);
+    if (lane == 0 && g_rows_stamps) {
+        unsigned long long* o = g_rows_stamps + ((int64_t)blockIdx.x * RW + wave) * 8;
+        o[0] = st_wait; o[1] = st_bar; o[2] = st_epi; o[3] = st_dma; o[4] = st_mfma; o[5] = st_end - st_begin;
+        o[6] = (unsigned long long)nc; o[7] = loader ? 1 : 0;
+    }
+#endif
 }
 
 template <int KS>
@@ -343,3 +380,9 @@ bool try_rows_x3(const GemmParams& p, int batch, int epi, hipStream_t s, int* rc
 }
 
 }  // namespace vasr
+
+#ifdef VASR_ROWS_STAMPS
+VASR_API int vasr_diag_rows_stamps(void* buf) {  // diagnostic builds only
+    return hipMemcpyToSymbol(HIP_SYMBOL(vasr::g_rows_stamps), &buf, sizeof(buf)) == hipSuccess ? VASR_OK : VASR_EINVAL;
+}
+#endif
