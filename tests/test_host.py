@@ -211,3 +211,41 @@ def test_tree_scan_kernel_mode_selection(monkeypatch):
     monkeypatch.setenv("VASR_SCAN_FMA", "1")
     assert ssm._tree_mode() == 2
     assert ssm._SCAN_MODE_ID == {"parallel": 0, "sequential": 1, "mamba": 1}
+
+
+def test_stft_kernel_has_no_packed_fp32_valu():
+    """The |STFT|^2 kernel is built without SLP vectorisation (velocity-asr_amd/Makefile): its
+    packed-fp32 form (v_pk_{mul,fma,add}_f32 with operand swaps) returned wrong values in one
+    half-wave beside tile GEMMs of another stream (profiles/r04l-r04o).  Checked on
+    the built library's gfx950 code object, here on the host."""
+    import shutil
+    import subprocess
+    import tempfile
+    from velocity_asr import _lib
+    llvm = "/opt/rocm/lib/llvm/bin"
+    objdump = os.path.join(llvm, "llvm-objdump")
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump absent")
+    with tempfile.TemporaryDirectory() as d:
+        lib = os.path.join(d, "lib.so")
+        shutil.copy(_lib.LIB_PATH, lib)
+        subprocess.run([objdump, "--offloading", lib], cwd=d, check=True, capture_output=True)
+        objs = [os.path.join(d, f) for f in os.listdir(d) if f.endswith("gfx950")]
+        assert objs, "no gfx950 code object in the library"
+        body, found = [], False
+        for o in objs:
+            out = subprocess.run([objdump, "-d", o], check=True, capture_output=True, text=True).stdout
+            for line in out.splitlines():
+                if "stft_power_400_kernel" in line and line.rstrip().endswith(">:"):
+                    found = True
+                    body = []
+                    continue
+                if found:
+                    body.append(line)
+                    if "s_endpgm" in line:
+                        break
+            if found:
+                break
+    assert found and len(body) > 100, "stft_power_400_kernel not found in the library"
+    packed = [ln.strip() for ln in body if any(op in ln for op in ("v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32"))]
+    assert not packed, packed[:4]
