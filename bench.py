@@ -407,14 +407,22 @@ def run(args):
     # RCCL joins after the graph streams exist: HIP deals streams round-robin onto the
     # process's few hardware queues (GPU_MAX_HW_QUEUES = 4), and a communicator created first
     # takes queues in that rotation so that the two utterance-group streams can land on one
-    # queue and serialise (measured 4.0 vs 2.7 ms per step)
-    if distributed:
+    # queue and serialise (measured 4.0 vs 2.7 ms per step).  With one rank nothing in the timed
+    # leg needs a communicator, and its mere presence cost the graph replays 2.2 % (150.4k vs
+    # 153.8k RTFx, profiles/r04ad/): the single rank joins after its timed leg, for the serving
+    # leg only.
+    def join_rccl():
         with stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator creation
             dist.init_process_group("nccl", device_id=dev)
             dist.barrier()
+    if distributed and world > 1:
+        join_rccl()
     for _ in range(args.warmup):
         step()
     elapsed = timed(step, args.steps, world, dev)
+
+    if distributed and world == 1:
+        join_rccl()
 
     # the tokens the timed graph wrote in its last replay vs the reference's greedy lists for the
     # same clips, and an eager pass over the same audio checked the same way (outside the timed
