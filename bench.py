@@ -8,13 +8,14 @@ collapse, on audio already resident in HBM, replayed as HIP graphs.
 
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` without WORLD_SIZE starts
 `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child process (before
-anything touches the GPU) and exits with its code; under torchrun every rank joins an RCCL
-("nccl") process group, world size 1 included.  Each rank transcribes its own 32 clips
+anything touches the GPU) and exits with its code.  Each rank transcribes its own 32 clips
 (utterance sharding, no data-path collective; weak scaling); a barrier + synchronize brackets
-the K timed steps and the max time over ranks is used.  A second timed leg ("with_scatter")
-runs the serving form: rank 0 holds the whole (N*32, S) batch in HBM, each step scatters the
-shards over RCCL (xGMI) straight into every rank's graph input, replays, and gathers the int32
-tokens back to rank 0 (velocity_asr.distributed.transcribe_sharded).
+the K timed steps and the max time over ranks is used -- barriers and max in a gloo process
+group on the host (an RCCL communicator's mere presence slowed the replays 2.2 %).  A second
+timed leg ("with_scatter") runs the serving form over an RCCL ("nccl") group joined after the
+first: rank 0 holds the whole (N*32, S) batch in HBM, each step scatters the shards over RCCL
+(xGMI) straight into every rank's graph input, replays, and gathers the int32 tokens back to
+rank 0 (velocity_asr.distributed.transcribe_sharded).
 
 Prints ONE JSON line (rank 0):
   value         = RTFx = audio seconds transcribed by all ranks / wall seconds (resident inputs)
@@ -349,7 +350,7 @@ def timed(step, steps, world, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)  # the timing group is gloo (host)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -359,7 +360,9 @@ def run(args):
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    dev = torch.device("cuda", local)
+    # VASR_BENCH_DEVICE pins every rank to one device index (rehearsing N ranks on a one-GPU box
+    # with --no-scatter; RCCL refuses two ranks on one GPU)
+    dev = torch.device("cuda", int(os.environ.get("VASR_BENCH_DEVICE", local)))
     torch.cuda.set_device(dev)
     distributed = "WORLD_SIZE" in os.environ
 
@@ -404,25 +407,20 @@ def run(args):
         tr.audio.copy_(audio)
         step = tr.step
 
-    # RCCL joins after the graph streams exist: HIP deals streams round-robin onto the
-    # process's few hardware queues (GPU_MAX_HW_QUEUES = 4), and a communicator created first
-    # takes queues in that rotation so that the two utterance-group streams can land on one
-    # queue and serialise (measured 4.0 vs 2.7 ms per step).  With one rank nothing in the timed
-    # leg needs a communicator, and its mere presence cost the graph replays 2.2 % (150.4k vs
-    # 153.8k RTFx, profiles/r04ad/): the single rank joins after its timed leg, for the serving
-    # leg only.
-    def join_rccl():
-        with stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator creation
-            dist.init_process_group("nccl", device_id=dev)
+    # The resident leg has no data-path collective (each rank transcribes its own shard), so its
+    # barriers and the max over ranks run in a gloo group on the host: an RCCL communicator's mere
+    # presence cost the graph replays 2.2 % (150.4k vs 153.8k RTFx at one rank,
+    # profiles/r04ad/).  RCCL joins after the timed leg, for the serving leg's scatter / gather --
+    # and after the graph streams exist: HIP deals streams round-robin onto the process's few
+    # hardware queues (GPU_MAX_HW_QUEUES = 4), and a communicator created first took queues so
+    # that the two utterance-group streams landed on one and serialised (4.0 vs 2.7 ms per step).
+    if distributed:
+        with stdout_to_stderr():  # gloo prints its connection line on stdout
+            dist.init_process_group("gloo")
             dist.barrier()
-    if distributed and world > 1:
-        join_rccl()
     for _ in range(args.warmup):
         step()
     elapsed = timed(step, args.steps, world, dev)
-
-    if distributed and world == 1:
-        join_rccl()
 
     # the tokens the timed graph wrote in its last replay vs the reference's greedy lists for the
     # same clips, and an eager pass over the same audio checked the same way (outside the timed
@@ -432,18 +430,18 @@ def run(args):
     toks, lens = (t.clone() for t in tr.collect()) if tr is not None else (etoks, elens)
     graph_match = token_lists(toks, lens) == token_lists(etoks, elens)
     if world > 1:  # every rank's graph tokens against its eager pass
-        bad = torch.tensor([0.0 if graph_match else 1.0], device=dev, dtype=torch.float64)
+        bad = torch.tensor([0.0 if graph_match else 1.0], dtype=torch.float64)
         dist.all_reduce(bad)
         graph_match = bad.item() == 0
     gc = torch.tensor(golden_check(toks, lens, args, rank) + golden_check(etoks, elens, args, rank),
-                      device=dev, dtype=torch.float64)
+                      dtype=torch.float64)
     if world > 1:
         dist.all_reduce(gc)
     gc = [int(v) for v in gc.tolist()]
     golden, golden_eager = golden_summary(gc[:7], args), golden_summary(gc[7:], args)
     valid = torch.arange(toks.shape[1], device=dev)[None, :] < lens[:, None]
     csum = torch.tensor([float(lens.sum().item()), float(toks.long().masked_fill(~valid, 0).sum().item())],
-                        device=dev, dtype=torch.float64)
+                        dtype=torch.float64)
     if world > 1:
         dist.all_reduce(csum)
 
@@ -451,6 +449,9 @@ def run(args):
     scatter = None
     if distributed and tr is not None and not args.no_scatter:
         from velocity_asr.distributed import graphed_step, transcribe_sharded
+        with stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator creation
+            rccl = dist.new_group(backend="nccl")
+            dist.barrier(group=rccl, device_ids=[local])
         full = None
         if rank == 0:
             full = torch.cat([torch.from_numpy(S.make_audio(B, S_len, seed=1234 + r)) for r in range(world)]).to(dev)
@@ -458,7 +459,8 @@ def run(args):
         res = {}
 
         def sstep():
-            res["out"] = transcribe_sharded(gstep, full, world * B, S_len, dev, shard=tr.audio, as_lists=False)
+            res["out"] = transcribe_sharded(gstep, full, world * B, S_len, dev, shard=tr.audio, as_lists=False,
+                                            group=rccl)
         for _ in range(max(2, args.warmup // 2)):
             sstep()
         el_s = timed(sstep, args.steps, world, dev)
@@ -558,7 +560,7 @@ def run(args):
                                f"{', INT8 fake-quant' if args.int8 else ''}"
                                f"{f', HIP graph x{streams} streams' if not args.eager else ', eager'})",
                    "global_batch": world * B, "clip_seconds": args.seconds, "schedule": schedule,
-                   "parallelism": f"utterance-shard x{world} over RCCL ({'resident shards; serving leg scatters from rank 0 and gathers tokens' if scatter else 'resident shards'})"
+                   "parallelism": f"utterance-shard x{world}, timing barriers over gloo, serving leg over RCCL ({'resident shards; serving leg scatters from rank 0 and gathers tokens' if scatter else 'resident shards'})"
                    if distributed else "single process"},
         "frames_per_sec": round(frames / elapsed, 1),
         "roofline": roof,

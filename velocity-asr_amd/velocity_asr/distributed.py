@@ -30,10 +30,11 @@ def shard_range(n: int, world: int, rank: int) -> Tuple[int, int]:
 
 
 def scatter_audio(audio: Optional[torch.Tensor], per_rank: int, samples: int, device: torch.device,
-                  src: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  src: int = 0, out: Optional[torch.Tensor] = None, group=None) -> torch.Tensor:
     """Scatter (world*per_rank, samples) audio held by `src` into (per_rank, samples) shards.
-    out: the destination shard (e.g. a GraphedTranscriber's static input), else allocated."""
-    world = dist.get_world_size()
+    out: the destination shard (e.g. a GraphedTranscriber's static input), else allocated.
+    group: the process group to use (default: the default group; every rank a member)."""
+    world = dist.get_world_size(group)
     if out is None:
         out = torch.empty((per_rank, samples), dtype=torch.float32, device=device)
     elif tuple(out.shape) != (per_rank, samples) or out.dtype != torch.float32 or not out.is_contiguous():
@@ -42,33 +43,34 @@ def scatter_audio(audio: Optional[torch.Tensor], per_rank: int, samples: int, de
         if audio is None or audio.shape != (world * per_rank, samples):
             raise ValueError(f"scatter_audio: src needs ({world * per_rank}, {samples}) audio")
         chunks = list(audio.to(device=device, dtype=torch.float32).contiguous().chunk(world, 0))
-        dist.scatter(out, chunks, src=src)
+        dist.scatter(out, chunks, src=src, group=group)
     else:
-        dist.scatter(out, None, src=src)
+        dist.scatter(out, None, src=src, group=group)
     return out
 
 
-def gather_token_blocks(tokens: torch.Tensor, lengths: torch.Tensor,
-                        dst: int = 0) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
+def gather_token_blocks(tokens: torch.Tensor, lengths: torch.Tensor, dst: int = 0,
+                        group=None) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
     """Gather per-rank (b, L) int32 tokens + (b,) lengths into (world*b, L) / (world*b,) device
     tensors on `dst` (rank order = utterance order); None on the other ranks."""
-    world = dist.get_world_size()
+    world = dist.get_world_size(group)
     tok = tokens.contiguous()
     ln = lengths.contiguous()
     if dist.get_rank() == dst:
         tok_all = torch.empty((world * tok.shape[0],) + tuple(tok.shape[1:]), dtype=tok.dtype, device=tok.device)
         len_all = torch.empty((world * ln.shape[0],), dtype=ln.dtype, device=ln.device)
-        dist.gather(tok, list(tok_all.chunk(world, 0)), dst=dst)
-        dist.gather(ln, list(len_all.chunk(world, 0)), dst=dst)
+        dist.gather(tok, list(tok_all.chunk(world, 0)), dst=dst, group=group)
+        dist.gather(ln, list(len_all.chunk(world, 0)), dst=dst, group=group)
         return tok_all, len_all
-    dist.gather(tok, None, dst=dst)
-    dist.gather(ln, None, dst=dst)
+    dist.gather(tok, None, dst=dst, group=group)
+    dist.gather(ln, None, dst=dst, group=group)
     return None
 
 
-def gather_tokens(tokens: torch.Tensor, lengths: torch.Tensor, dst: int = 0) -> Optional[List[List[int]]]:
+def gather_tokens(tokens: torch.Tensor, lengths: torch.Tensor, dst: int = 0,
+                  group=None) -> Optional[List[List[int]]]:
     """Gather per-rank (b, L) int32 tokens + (b,) lengths on `dst`; returns lists there, else None."""
-    blocks = gather_token_blocks(tokens, lengths, dst)
+    blocks = gather_token_blocks(tokens, lengths, dst, group)
     if blocks is None:
         return None
     t, n = blocks[0].cpu(), blocks[1].cpu()
@@ -77,20 +79,21 @@ def gather_tokens(tokens: torch.Tensor, lengths: torch.Tensor, dst: int = 0) -> 
 
 def transcribe_sharded(step: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],
                        audio: Optional[torch.Tensor], batch: int, samples: int, device: torch.device,
-                       src: int = 0, shard: Optional[torch.Tensor] = None, as_lists: bool = True):
+                       src: int = 0, shard: Optional[torch.Tensor] = None, as_lists: bool = True, group=None):
     """Scatter `batch` clips from `src`, run `step(shard) -> (tokens, lengths)` on every rank,
     gather the results on `src`: token lists, or with as_lists=False the (batch, L) / (batch,)
     device tensors.  `batch` must divide by the world size (equal shards: the model has no
     padding masks, so utterances are never padded to a common length).  shard: the buffer to
-    scatter into (a GraphedTranscriber's static input; see graphed_step)."""
-    world = dist.get_world_size()
+    scatter into (a GraphedTranscriber's static input; see graphed_step).  group: the process
+    group of the collectives (default: the default group)."""
+    world = dist.get_world_size(group)
     if batch % world:
         raise ValueError(f"batch {batch} must be a multiple of the world size {world}")
-    shard = scatter_audio(audio, batch // world, samples, device, src, out=shard)
+    shard = scatter_audio(audio, batch // world, samples, device, src, out=shard, group=group)
     tokens, lengths = step(shard)
     if as_lists:
-        return gather_tokens(tokens, lengths, src)
-    return gather_token_blocks(tokens, lengths, src)
+        return gather_tokens(tokens, lengths, src, group)
+    return gather_token_blocks(tokens, lengths, src, group)
 
 
 def hip_step(model) -> Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]:
