@@ -10,7 +10,8 @@ from velocity_asr import synthetic as S
 from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids, token_lists
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "caller"
-B, NB, REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 2, 16, 25
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+NB, REPS = int(os.environ.get("STRESS_NB", 16)), int(os.environ.get("STRESS_REPS", 25))  # builds, replays per build
 dev = torch.device("cuda", 0)
 m = va.VELOCITYASR()
 m.load_state_dict({k: torch.from_numpy(v) for k, v in S.make_weights(None, seed=0).items()}, strict=True)
