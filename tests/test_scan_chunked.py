@@ -55,7 +55,8 @@ def _form(form, fn, *a):
 @pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("npl", [2, 4])
 @pytest.mark.parametrize("tc", [16, 32])
-@pytest.mark.parametrize("B,L", [(1, 1), (1, 17), (2, 17), (1, 501), (2, 501), (1, 1501), (2, 2049), (1, 4100), (1, 8192)])
+@pytest.mark.parametrize("B,L", [(1, 1), (1, 17), (2, 17), (1, 257), (1, 501), (2, 501), (1, 512), (1, 513), (1, 1501),
+                                 (2, 2049), (1, 4100), (1, 8192)])
 def test_chunked_bitwise_equals_streaming(mode, npl, tc, B, L):
     """The chunk-parallel form equals the streaming kernel bit for bit, with either streaming
     chunk length (16 / 32 steps: the same float operations) and either lane layout."""
