@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../velocity-asr_amd"
 OUT=../tools/_variants/$NAME; mkdir -p "$OUT"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -munsafe-fp-atomics $*"
 for f in csrc/*.hip csrc/*.cpp; do
-  extra=""; case "$(basename $f)" in scan*.hip) extra="-fno-slp-vectorize -ffp-contract=off";; esac
+  extra=""; case "$(basename $f)" in scan*.hip) extra="-fno-slp-vectorize -ffp-contract=off";; stft.hip) extra="-fno-slp-vectorize";; esac
   stem=$(basename $f); stem=${stem%.*}; v="EXTRA_$stem"; extra="$extra ${!v:-}"
   /opt/rocm/bin/hipcc $FLAGS $extra -c "$f" -o "$OUT/$(basename $f).o" &
   pids="$pids $!"
