@@ -50,12 +50,21 @@ constexpr int NSTAGES = 36;      // out_proj 12 k-steps, FFN1 2 halves x 6, FFN2
 #define VASR_TAIL_PD16 2  // the 16-row form (two waves per SIMD: 256 registers, no spills at 2)
 #endif
 #ifndef VASR_TAIL_PD12
-#define VASR_TAIL_PD12 6  // 12 waves (one column tile each), 16 rows: 168 registers, no spills
+#define VASR_TAIL_PD12 4  // 12 waves (one column tile each), 16 rows: 154 registers (5: 168, within 0.3 us)
+#endif
+// Diagnostic ablations (tools/build_variant_lib.sh -DVASR_TAIL_ABLATE=<bits>; results wrong):
+// 1 = no weight loads after the prologue's, 2 = no MFMAs (one add per tile keeps the loads
+// live), 4 = no A-fragment LDS reads in the steps
+#ifndef VASR_TAIL_ABLATE
+#define VASR_TAIL_ABLATE 0
+#endif
+#ifndef VASR_TAIL_PD21
+#define VASR_TAIL_PD21 2  // 32 rows, 12 waves: 168 registers with the A fragments pipelined (3: spills)
 #endif
 template <int NP, int RT = 2, int CT = 3>
 constexpr int pd_of() {
     if constexpr (NP == 1) return CT == 3 ? 6 : 8;
-    if constexpr (CT == 1) return RT == 1 ? VASR_TAIL_PD12 : 4;
+    if constexpr (CT == 1) return RT == 1 ? VASR_TAIL_PD12 : VASR_TAIL_PD21;
     if constexpr (CT == 2) return 3;
     return RT == 1 ? VASR_TAIL_PD16 : VASR_TAIL_PD;
 }
@@ -96,6 +105,7 @@ struct TailCtx {
     char* H;   // 192-wide planes (h)
     int lane, wave, r, q, m0;
     floatx4 acc[RT][CT];
+    bf16x8 a[2][RT][NP];  // A fragments of this step and the next
     bf16x8 w[RING][CT][NP];  // [ring slot][column tile][plane]
     float x1[RT][CT][4];     // residual x, then x1 = out_proj(g) + x
     float bb1[2][CT], bb2[CT], lnw[3], lnb[3];
@@ -132,27 +142,54 @@ __device__ __forceinline__ void load_first(TailCtx<NP, RT, CT>& c) {
 }
 
 template <int S, int NP, int RT, int CT>
-__device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
+__device__ __forceinline__ void read_step_a(TailCtx<NP, RT, CT>& c, bf16x8 (&a)[RT][NP]) {
     using Ctx = TailCtx<NP, RT, CT>;
-    constexpr int PD = Ctx::PD;
-    if constexpr (S + PD < NSTAGES) load_w<S + PD, NP, RT, CT>(c);
-    // keep the prefetch where it is: without this fence the scheduler sinks the loads next to
-    // their use (to save registers) and the step then waits on them (measured: the weight
-    // stream then ran at a third of the L2 rate)
-    __builtin_amdgcn_sched_barrier(0);
-    // A fragments of both row tiles
-    bf16x8 a[RT][NP];
 #pragma unroll
     for (int tm = 0; tm < RT; ++tm) {
+        if constexpr ((VASR_TAIL_ABLATE & 4) != 0) {
+#pragma unroll
+            for (int pl = 0; pl < NP; ++pl) a[tm][pl] = c.w[(S + 1) % Ctx::RING][0][pl];
+            continue;
+        }
         if constexpr (S < 12 || S >= 24)
             read_a<NP, TE, Ctx::ROWS>(c.R, 16 * tm + c.r, S < 12 ? S : S - 24, c.q, a[tm]);
         else
             read_a<NP, TD, Ctx::ROWS>(c.H, 16 * tm + c.r, (S - 12) % 6, c.q, a[tm]);
     }
+}
+
+template <int S, int NP, int RT, int CT>
+__device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
+    using Ctx = TailCtx<NP, RT, CT>;
+    constexpr int PD = Ctx::PD;
+    if constexpr (S + PD < NSTAGES && !(VASR_TAIL_ABLATE & 1)) load_w<S + PD, NP, RT, CT>(c);
+    // keep the prefetch where it is: without this fence the scheduler sinks the loads next to
+    // their use (to save registers) and the step then waits on them (measured: the weight
+    // stream then ran at a third of the L2 rate)
+    __builtin_amdgcn_sched_barrier(0);
+    // A fragments of both row tiles, read one step ahead of their MFMAs: the next step's are
+    // issued before this step's products (whose fragments were read a step earlier), so an LDS
+    // round trip no longer sits in front of every step's first MFMA.  Steps 0, 12 and 24 start a
+    // product whose A image is written at the end of the step before (LN at 11, f at 23): they
+    // read their own.  Measured (graph-timed, profiles/r04ap, r04aq): the A reads were the
+    // largest single cost of a step -- without them the M = 501 launch took 8.9 instead of 15.9
+    // us -- and pipelining them took it to 13.4 us (12 waves), M = 16032 from 50 to 48 us;
+    // bitwise the same outputs.
+    constexpr bool first = S == 0 || S == 12 || S == 24;
+    if constexpr (first) read_step_a<S, NP, RT, CT>(c, c.a[S & 1]);
+    if constexpr (S + 1 < NSTAGES && S + 1 != 12 && S + 1 != 24) read_step_a<S + 1, NP, RT, CT>(c, c.a[(S + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of this step's MFMAs
+    auto& a = c.a[S & 1];
 #pragma unroll
     for (int tm = 0; tm < RT; ++tm)
 #pragma unroll
-        for (int t = 0; t < CT; ++t) c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % Ctx::RING][t], c.acc[tm][t]);
+        for (int t = 0; t < CT; ++t) {
+            if constexpr ((VASR_TAIL_ABLATE & 2) != 0) {
+                c.acc[tm][t][0] += (float)c.w[S % Ctx::RING][t][0][0] + (float)a[tm][0][1];
+                continue;
+            }
+            c.acc[tm][t] = mac_tile<NP>(a[tm], c.w[S % Ctx::RING][t], c.acc[tm][t]);
+        }
 
     if constexpr (S == 11) {
         // x1 = out_proj(g) + x (registers, kept for the final residual) -> fp32 scratch in R
@@ -334,12 +371,13 @@ int tail_rows(int M) {
 
 // Waves per workgroup (12 / column tiles per wave).  At 32 rows, 12 waves of one column tile
 // each take 23.3 vs 26.2 us at M = 8016 (profiles/r03m/tail.txt: the block's MFMA chain split
-// three ways per SIMD); 16-row blocks do not gain (18-19 us for any wave count: the per-CU L2
-// weight stream, 1.3 MB per block at ~70 GB/s, sets their time).  vasr_set_option(
-// VASR_OPT_TAIL_WAVES, 4|6|12) (env VASR_TAIL_WAVES) forces one.
+// three ways per SIMD).  16-row blocks too, graph-timed: 13.4 vs 15.8 us at M = 501, 13.7 vs
+// 16.2 at M = 1024 (profiles/r04aq; round 2's "no gain" had timed the Python call path, which
+// at these sizes is slower than the kernel).  vasr_set_option(VASR_OPT_TAIL_WAVES, 4|6|12) (env
+// VASR_TAIL_WAVES) forces one.
 int tail_waves(int M) {
     if (const int w = option(VASR_OPT_TAIL_WAVES)) return w;
-    return tail_rows(M) == 32 ? 12 : 4;
+    return 12;
 }
 
 template <int NP>
