@@ -337,6 +337,41 @@ def pmc_lookup(name, key=None):
         return None
 
 
+def agree_max_over_ranks(times):
+    """The schedule timings every rank decides on: each candidate's max over ranks (the timed
+    value is the max over ranks, so the schedule whose slowest rank is fastest wins); gloo group."""
+    keys = sorted(times)
+    t = torch.tensor([times[k] for k in keys], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {k: float(v) for k, v in zip(keys, t.tolist())}
+
+
+def schedule_how(tried, world):
+    if not tried:
+        return "single candidate (batch under 8 clips or odd): one graph"
+    how = (f"{len(tried)} schedules built and timed on the bench's own audio in the untimed warm-up "
+           f"(5 replays x 2 rounds each); the faster kept")
+    if world > 1:
+        how += "; times are the max over ranks, so every rank keeps the same schedule"
+    return how
+
+
+def run_verdict(graph_match, golden, warm_golden, golden_eager):
+    """(exit code, reasons): the line is invalid when the timed graphs' tokens differ from an eager
+    pass, or when the timed graphs' (last timed or last warm-up replay) or the eager pass's token
+    lists fail the reference check (tokens_vs_reference.all_ranks_pass false)."""
+    why = []
+    if not graph_match:
+        why.append("the timed graphs' tokens differ from an eager pass over the same audio "
+                   "(graph_tokens_match_eager false)")
+    for name, g in (("tokens_vs_reference", golden), ("warmup_tokens_vs_reference", warm_golden),
+                    ("eager_tokens_vs_reference", golden_eager)):
+        if g is not None and not g.get("all_ranks_pass", False):
+            why.append(f"{name}.all_ranks_pass is false ({g.get('clips_identical')} of {g.get('clips')} clips "
+                       f"identical, token edit rate {g.get('token_edit_rate')})")
+    return (1 if why else 0), why
+
+
 def timed(step, steps, world, dev):
     torch.cuda.synchronize()
     if world > 1:
@@ -362,9 +397,12 @@ def run(args):
     local = int(os.environ.get("LOCAL_RANK", 0))
     # VASR_BENCH_DEVICE pins every rank to one device index (rehearsing N ranks on a one-GPU box
     # with --no-scatter; RCCL refuses two ranks on one GPU)
+    distributed = "WORLD_SIZE" in os.environ
+    if "VASR_BENCH_DEVICE" in os.environ and world > 1 and not args.no_scatter:
+        log("bench.py: VASR_BENCH_DEVICE pins every rank to one GPU, which RCCL refuses; add --no-scatter")
+        return 2
     dev = torch.device("cuda", int(os.environ.get("VASR_BENCH_DEVICE", local)))
     torch.cuda.set_device(dev)
-    distributed = "WORLD_SIZE" in os.environ
 
     from velocity_asr import synthetic as S
     from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids
@@ -390,6 +428,19 @@ def run(args):
     schedule = None
     audio = torch.from_numpy(S.make_audio(B, S_len, seed=1234 + rank)).to(dev)  # resident in HBM
 
+    # The resident leg has no data-path collective (each rank transcribes its own shard), so its
+    # barriers, the max over ranks and the schedule agreement run in a gloo group on the host: an
+    # RCCL communicator's mere presence cost the graph replays 2.2 % (150.4k vs 153.8k RTFx at one
+    # rank, profiles/r04ad/).  RCCL joins after the timed leg, for the serving leg's scatter /
+    # gather -- and after the graph streams exist: HIP deals streams round-robin onto the
+    # process's few hardware queues (GPU_MAX_HW_QUEUES = 4), and a communicator created first took
+    # queues so that the two utterance-group streams landed on one and serialised (4.0 vs 2.7 ms
+    # per step).
+    if distributed:
+        with stdout_to_stderr():  # gloo prints its connection line on stdout
+            dist.init_process_group("gloo")
+            dist.barrier()
+
     if args.eager:
         def step():
             return audio_to_token_ids(model, audio)
@@ -399,27 +450,24 @@ def run(args):
             tr = GraphedTranscriber(model, B, S_len, dev, streams=streams)
         else:
             from velocity_asr.pipeline import autotuned_transcriber
-            tr, tried = autotuned_transcriber(model, B, S_len, dev)
+            tr, tried = autotuned_transcriber(model, B, S_len, dev, audio=audio,
+                                              agree=agree_max_over_ranks if world > 1 else None)
             streams = len(tr.graphs)
-            schedule = dict(chosen_streams=streams, ms_per_replay_by_streams=tried,
-                            how="both schedules built and timed in the untimed warm-up (5 replays x 2 rounds each); "
-                                "the faster kept")
+            schedule = dict(chosen_streams=streams, ms_per_replay_by_streams=tried, how=schedule_how(tried, world))
         tr.audio.copy_(audio)
         step = tr.step
 
-    # The resident leg has no data-path collective (each rank transcribes its own shard), so its
-    # barriers and the max over ranks run in a gloo group on the host: an RCCL communicator's mere
-    # presence cost the graph replays 2.2 % (150.4k vs 153.8k RTFx at one rank,
-    # profiles/r04ad/).  RCCL joins after the timed leg, for the serving leg's scatter / gather --
-    # and after the graph streams exist: HIP deals streams round-robin onto the process's few
-    # hardware queues (GPU_MAX_HW_QUEUES = 4), and a communicator created first took queues so
-    # that the two utterance-group streams landed on one and serialised (4.0 vs 2.7 ms per step).
-    if distributed:
-        with stdout_to_stderr():  # gloo prints its connection line on stdout
-            dist.init_process_group("gloo")
-            dist.barrier()
     for _ in range(args.warmup):
         step()
+    # the warm-up's last replay checked against the reference too (not only the timed leg's last)
+    warm_golden = None
+    if tr is not None:
+        torch.cuda.synchronize()
+        wt, wl = (t.clone() for t in tr.collect())
+        wc = torch.tensor(golden_check(wt, wl, args, rank), dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(wc)
+        warm_golden = golden_summary([int(v) for v in wc.tolist()], args)
     elapsed = timed(step, args.steps, world, dev)
 
     # the tokens the timed graph wrote in its last replay vs the reference's greedy lists for the
@@ -451,7 +499,7 @@ def run(args):
         from velocity_asr.distributed import graphed_step, transcribe_sharded
         with stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator creation
             rccl = dist.new_group(backend="nccl")
-            dist.barrier(group=rccl, device_ids=[local])
+            dist.barrier(group=rccl, device_ids=[dev.index])
         full = None
         if rank == 0:
             full = torch.cat([torch.from_numpy(S.make_audio(B, S_len, seed=1234 + r)) for r in range(world)]).to(dev)
@@ -479,6 +527,8 @@ def run(args):
 
     rf = kernel_roofline(model, audio, args.roofline_steps, 1 if args.eager else streams)
     iso = isolated_times(model, audio[:B // (1 if args.eager else streams)])  # one utterance group's launch shape
+    from velocity_asr.ops import probe_clock
+    machine = probe_clock(dev)  # right after the isolated launches: the clock they ran at, XCD dispatch order
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -563,6 +613,7 @@ def run(args):
                    "parallelism": f"utterance-shard x{world}, timing barriers over gloo, serving leg over RCCL ({'resident shards; serving leg scatters from rank 0 and gathers tokens' if scatter else 'resident shards'})"
                    if distributed else "single process"},
         "frames_per_sec": round(frames / elapsed, 1),
+        "machine": machine,
         "roofline": roof,
         "with_scatter": scatter,
         "kernels": {
@@ -577,6 +628,7 @@ def run(args):
         "graph_tokens_match_eager": graph_match,
         "rank0_tokens_match_reference": None if golden is None else bool(golden["all_ranks_pass"]),
         "tokens_vs_reference": golden,
+        "warmup_tokens_vs_reference": warm_golden,
         "eager_tokens_vs_reference": golden_eager,
     }
     if world == 1 and not args.no_cpu_baseline:
@@ -584,11 +636,10 @@ def run(args):
     print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()
-    if not graph_match:  # the timed graphs' tokens differ from an eager pass: the line is not valid
-        log("bench.py: the timed graphs' tokens differ from an eager pass over the same audio "
-            "(graph_tokens_match_eager false); failing the run")
-        return 1
-    return 0
+    rc, why = run_verdict(graph_match, golden, warm_golden, golden_eager)
+    for w in why:
+        log(f"bench.py: {w}; failing the run")
+    return rc
 
 
 def main():

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 12
+#define VASR_ABI_VERSION 13
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -54,6 +54,14 @@ enum vasr_option {
     VASR_OPT_TAIL_WAVES = 4   /* waves per fused-SSMBlock-tail workgroup: 0, 4, 6, 12 (VASR_TAIL_WAVES)    */
 };
 int vasr_set_option(int key, int value);
+
+/* Diagnostics (no reference counterpart; bench.py's machine-state record).  A `blocks`-workgroup
+ * launch of 256 threads, each running a dependent VALU chain of `iters` steps; per workgroup b:
+ * out[3b] = the XCD (XCC_ID hardware register) it ran on, out[3b + 1] / out[3b + 2] = the shader
+ * clock (s_memtime) / 100-MHz constant (s_memrealtime) ticks its wave 0 spent in the chain.  The
+ * clock is out[3b+1] / out[3b+2] * 100 MHz; out[3b] == b % 8 checks the round-robin XCD dispatch
+ * the kernels' XCD-aware block maps assume.  out: device, 3 * blocks int64. */
+int vasr_probe_clock(int64_t* out, int blocks, int iters, void* stream);
 
 /* ------------------------------------------------------------------ GEMM
  * C[b] = epilogue(A[b] (M x K) * W^T (K x N) + bias), W row-major [N][K] as in

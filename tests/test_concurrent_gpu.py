@@ -70,6 +70,27 @@ def test_two_one_clip_groups_match_eager(model):
     assert not bad, f"(replay, clip) with tokens different from eager: {bad[:12]}"
 
 
+def test_two_one_clip_groups_stress_800_replays(model):
+    """The same two concurrent 1-clip groups, 800 replays, each replay's token block and lengths
+    compared with eager's on the device (the race the removed SERIAL_MAX_GROUP fallback covered
+    showed in about 1 of 100-200 replays; profiles/r04ah/ ran 800 and 2,000)."""
+    from velocity_asr.pipeline import GraphedTranscriber, audio_to_token_ids
+    audio = torch.from_numpy(S.make_audio(2, 160000, seed=4321)).to(DEV)
+    with torch.no_grad():
+        et, el = audio_to_token_ids(model, audio)
+    valid = torch.arange(et.shape[1], device=DEV)[None, :] < el[:, None]  # slots past a length are unspecified
+    et = et.masked_fill(~valid, 0)
+    tr = GraphedTranscriber(model, 2, 160000, streams=2)
+    tr.audio.copy_(audio)
+    bad = []
+    for r in range(800):
+        tr.step()
+        t, n = tr.collect()
+        if not (torch.equal(n, el) and torch.equal(t.masked_fill(~valid, 0), et)):
+            bad.append(r)
+    assert not bad, f"{len(bad)} of 800 replays differ from eager (first: {bad[:8]})"
+
+
 def test_scan_beside_coresident_gemms_is_bitwise_alone(model):
     """The local-block scan of 16 clips (the bench's group shape) launched 24 times on one stream
     while a tile-engine GEMM (M = 8016, N = 384) and the 16-row global tail run on another:
@@ -113,9 +134,9 @@ def test_autotuned_schedule_matches_eager(model):
     audio = torch.from_numpy(S.make_audio(8, 48000, seed=77)).to(DEV)
     with torch.no_grad():
         exp = token_lists(*audio_to_token_ids(model, audio))
-    tr, tried = autotuned_transcriber(model, 8, 48000, reps=2, rounds=1)
+    tr, tried = autotuned_transcriber(model, 8, 48000, reps=2, rounds=1, audio=audio)
     assert sorted(tried) == [1, 2] and len(tr.graphs) in (1, 2)
-    tr.audio.copy_(audio)
+    assert torch.equal(tr.audio, audio)  # timed on (and holding) the clips it serves
     for _ in range(3):
         tr.step()
         assert token_lists(*tr.collect()) == exp

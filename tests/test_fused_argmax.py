@@ -125,4 +125,8 @@ def test_graphed_transcriber_refuses_changed_weights(va):
     with pytest.raises(RuntimeError, match="changed after capture"):
         gt.collect()
     torch.cuda.synchronize()
-    assert (gt.lengths == -1).all()
+    # its static outputs are cleared: a caller holding the buffers sees empty transcripts
+    assert (gt.lengths == 0).all() and (gt.tokens == 0).all()
+    from velocity_asr.distributed import graphed_step
+    with pytest.raises(RuntimeError, match="changed after capture"):
+        graphed_step(gt)(gt.audio)

@@ -579,3 +579,12 @@ def test_gemm_rows_engine_bitwise_equals_tiles(va, M, N, K, epi):
         with ops.option(_lib.OPT_GEMM_ENGINE, eng):
             out[eng] = ops.gemm_argmax(a, w, b) if epi == "argmax" else ops.gemm(a, w, b, **kw)
     assert torch.equal(out[1], out[2])
+
+
+def test_probe_clock_reports_clock_and_xcd_dispatch(va):
+    """vasr_probe_clock (bench.py's machine record): a plausible shader clock and all 8 XCDs seen;
+    the round-robin fraction is reported, not asserted (it is what the probe measures)."""
+    from velocity_asr import ops
+    m = ops.probe_clock(torch.device(DEV), blocks=512, iters=4000)
+    assert 0.5 < m["clock_ghz"] < 3.5, m
+    assert m["xcds_seen"] == 8 and 0.0 <= m["xcd_round_robin_frac"] <= 1.0, m

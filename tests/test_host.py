@@ -6,6 +6,8 @@ tests are in test_gpu_parity.py (pytest -m gpu).
 
 import ctypes
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -213,39 +215,60 @@ def test_tree_scan_kernel_mode_selection(monkeypatch):
     assert ssm._SCAN_MODE_ID == {"parallel": 0, "sequential": 1, "mamba": 1}
 
 
-def test_stft_kernel_has_no_packed_fp32_valu():
-    """The |STFT|^2 kernel is built without SLP vectorisation (velocity-asr_amd/Makefile): its
-    packed-fp32 form (v_pk_{mul,fma,add}_f32 with operand swaps) returned wrong values in one
-    half-wave beside tile GEMMs of another stream (profiles/r04l-r04o).  Checked on
-    the built library's gfx950 code object, here on the host."""
-    import shutil
-    import subprocess
-    import tempfile
-    from velocity_asr import _lib
-    llvm = "/opt/rocm/lib/llvm/bin"
-    objdump = os.path.join(llvm, "llvm-objdump")
-    if not os.path.exists(objdump):
+def _isa_scan():
+    sys.path.insert(0, os.path.join(REPO, "tools", "isa"))
+    import isa_scan
+    try:
+        isa_scan.objdump()
+    except FileNotFoundError:
         pytest.skip("llvm-objdump absent")
-    with tempfile.TemporaryDirectory() as d:
-        lib = os.path.join(d, "lib.so")
-        shutil.copy(_lib.LIB_PATH, lib)
-        subprocess.run([objdump, "--offloading", lib], cwd=d, check=True, capture_output=True)
-        objs = [os.path.join(d, f) for f in os.listdir(d) if f.endswith("gfx950")]
-        assert objs, "no gfx950 code object in the library"
-        body, found = [], False
-        for o in objs:
-            out = subprocess.run([objdump, "-d", o], check=True, capture_output=True, text=True).stdout
-            for line in out.splitlines():
-                if "stft_power_400_kernel" in line and line.rstrip().endswith(">:"):
-                    found = True
-                    body = []
-                    continue
-                if found:
-                    body.append(line)
-                    if "s_endpgm" in line:
-                        break
-            if found:
-                break
-    assert found and len(body) > 100, "stft_power_400_kernel not found in the library"
-    packed = [ln.strip() for ln in body if any(op in ln for op in ("v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32"))]
+    return isa_scan
+
+
+@pytest.fixture(scope="module")
+def shipped_kernels():
+    from velocity_asr import _lib
+    return _isa_scan().library_kernels(_lib.LIB_PATH)
+
+
+def test_no_kernel_has_a_packed_fp32_op_with_swapped_source(shipped_kernels):
+    """Library-wide guard: no kernel in the shipped gfx950 code has a packed-fp32
+    VOP3P instruction (v_pk_{add,mul,fma}_f32) reading a source with its dwords swapped (op_sel 1,
+    op_sel_hi 0).  That form -- 12 instructions of stft.hip's SLP-vectorised build, the re/im swaps
+    of its complex products -- returned wrong |STFT|^2 values for a half-wave beside MFMA kernels of
+    another stream: 18/400 launches, 0/400 with only those 12 rewritten as scalar pairs, 18-19/400
+    with every other packed form rewritten instead (profiles/r05e/, r05f/)."""
+    isa = _isa_scan()
+    assert len(shipped_kernels) > 200
+    hits = {k: isa.pk_swapped(v) for k, v in shipped_kernels.items()}
+    hits = {k: h for k, h in hits.items() if h}
+    assert not hits, [(k[:80], h[0][1]) for k, h in list(hits.items())[:4]]
+
+
+def test_stft_kernel_has_no_packed_fp32_valu(shipped_kernels):
+    """stft.hip is built without SLP vectorisation (velocity-asr_amd/Makefile), so its kernel holds
+    no packed-fp32 VALU at all."""
+    body = [v for k, v in shipped_kernels.items() if "stft_power_400_kernel" in k]
+    assert body and len(body[0]) > 100, "stft_power_400_kernel not found in the library"
+    packed = [ln for ln in body[0] if ln.startswith(("v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32"))]
     assert not packed, packed[:4]
+
+
+def test_isa_guard_detects_the_slp_stft_sequence(tmp_path):
+    """Positive control of the guard: stft.hip compiled WITH SLP vectorisation (the build that
+    failed) has the form (12 instructions); the shipped flags (-fno-slp-vectorize) do not."""
+    isa = _isa_scan()
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc absent")
+    pkg = os.path.join(REPO, "velocity-asr_amd")
+    found = {}
+    for tag, extra in (("slp", []), ("noslp", ["-fno-slp-vectorize"])):
+        asm = tmp_path / f"{tag}.s"
+        subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "-I../include", "-munsafe-fp-atomics",
+                        "--cuda-device-only", "-S", "csrc/stft.hip", "-o", str(asm)] + extra,
+                       cwd=pkg, check=True, capture_output=True)
+        ins = [ln.strip() for ln in open(asm) if ln.startswith("\t") and not ln.strip().startswith((".", ";"))]
+        found[tag] = isa.pk_swapped(ins)
+    assert len(found["slp"]) >= 10, found["slp"]
+    assert found["noslp"] == []

@@ -68,7 +68,39 @@ def bits(t):
 
 
 VIC = os.environ.get("VICTIM")
-if VIC is None:
+HSACO = os.environ.get("VICTIM_HSACO")
+if HSACO:
+    # the victim is stft_power_400_kernel<6> from a standalone code object (tools/diag/stft_surgery.py),
+    # launched with hipModuleLaunchKernel on the current (capturing) stream into a fresh output
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    _mod, _fn = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipModuleLoad(ctypes.byref(_mod), HSACO.encode()) == 0, "hipModuleLoad"
+    _sym = os.environ.get("VICTIM_SYMBOL", "_ZN4vasr12_GLOBAL__N_121stft_power_400_kernelILi6EEEvPKfliPKiiS3_Pfll")
+    assert hip.hipModuleGetFunction(ctypes.byref(_fn), _mod, _sym.encode()) == 0, "hipModuleGetFunction"
+    print("victim: module", HSACO, flush=True)
+    _keep = []
+
+    def victim():
+        B, S = a1.shape
+        F = S // 160 + 1
+        power = torch.empty((B, F, 201), device=dev, dtype=torch.float32)
+        args = [ctypes.c_void_p(a1.data_ptr()), ctypes.c_int64(S), ctypes.c_int32(S), ctypes.c_void_p(0),
+                ctypes.c_int32(F), ctypes.c_void_p(tb.window.data_ptr()), ctypes.c_void_p(power.data_ptr()),
+                ctypes.c_int64(201), ctypes.c_int64(F * 201)]
+        params = (ctypes.c_void_p * len(args))(*[ctypes.cast(ctypes.byref(v), ctypes.c_void_p) for v in args])
+        _keep.append((args, params))
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        rc = hip.hipModuleLaunchKernel(_fn, (F + 5) // 6, B, 1, 256, 1, 1, 0, st, params, None)
+        assert rc == 0, f"hipModuleLaunchKernel {rc}"
+        return power
+    _lib_ref = orig["stft_power_400"](a1, tb.window)
+    _mod_out = victim()
+    torch.cuda.synchronize()
+    _d = (_mod_out - _lib_ref).abs().max().item()
+    print(f"module kernel alone vs the library kernel: max |diff| {_d:.3g}, bitwise equal "
+          f"{bool(torch.equal(_mod_out.view(torch.int32), _lib_ref.view(torch.int32)))}", flush=True)
+elif VIC is None:
     def victim():
         return orig["stft_power_400"](a1, tb.window)
 else:

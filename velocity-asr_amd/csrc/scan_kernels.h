@@ -227,6 +227,16 @@ __device__ __forceinline__ f2 mad2(f2 a, f2 b, f2 c) {
     }
 }
 
+// x + y as one scalar v_add_f32 (used where needed: at N = 128).  Left to itself the compiler
+// forms the sum of a pair's two halves there as v_pk_add_f32 with the second source's dwords swapped (op_sel:[0,1]
+// op_sel_hi:[1,0]): a packed-fp32 form that returned wrong values in a half-wave beside MFMA kernels
+// of another stream (profiles/r05e-r05f); tests/test_host.py checks every shipped kernel.
+__device__ __forceinline__ float add_f32(float x, float y) {
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
 __device__ __forceinline__ f2 exp2v(f2 v) {
     f2 r;
     r.x = __builtin_amdgcn_exp2f(v.x);

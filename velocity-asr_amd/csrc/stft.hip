@@ -66,9 +66,30 @@ constexpr TwTable make_twiddles() {
 }
 __constant__ constexpr TwTable kTw = make_twiddles();
 
+// Diagnostic builds only (tools/runs/r05c.sh): VASR_STFT_VGPR_CONSTS=1 holds the
+// DFT constants in VGPRs (opaque to the compiler), so an SLP-vectorised build has packed-fp32 ops
+// with VGPR operands only, instead of SGPR-pair operands.
+#ifndef VASR_STFT_VGPR_CONSTS
+#define VASR_STFT_VGPR_CONSTS 0
+#endif
+__device__ __forceinline__ float kconst(float c) {
+    if constexpr (VASR_STFT_VGPR_CONSTS) asm volatile("" : "+v"(c));
+    return c;
+}
+// VASR_STFT_OPAQUE_INDEX=1 hides the thread index's range from the compiler, so the stages' index
+// arithmetic (t / 25, t / 40, r / 5) is 32-bit, not the 16-bit SDWA / packed-u16 forms it
+// otherwise narrows to.
+#ifndef VASR_STFT_OPAQUE_INDEX
+#define VASR_STFT_OPAQUE_INDEX 0
+#endif
+__device__ __forceinline__ int kindex(int t) {
+    if constexpr (VASR_STFT_OPAQUE_INDEX) asm volatile("" : "+v"(t));
+    return t;
+}
+
 // Forward DFT-8 (radix-2, decimation in time), in place.
 __device__ __forceinline__ void dft8(cf (&v)[8]) {
-    const float r = 0.70710678118654752440f;
+    const float r = kconst(0.70710678118654752440f);
     const cf a0 = v[0] + v[4], a1 = v[0] - v[4], a2 = v[2] + v[6], a3 = v[2] - v[6];
     const cf a4 = v[1] + v[5], a5 = v[1] - v[5], a6 = v[3] + v[7], a7 = v[3] - v[7];
     const cf b0 = a0 + a2, b2 = a0 - a2, b1 = a1 + mul_mi(a3), b3 = a1 + mul_pi(a3);
@@ -87,8 +108,8 @@ __device__ __forceinline__ void dft8(cf (&v)[8]) {
 
 // Forward DFT-5, in place.
 __device__ __forceinline__ void dft5(cf (&v)[5]) {
-    const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
-    const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+    const float c1 = kconst(0.30901699437494742410f), c2 = kconst(-0.80901699437494742410f);
+    const float s1 = kconst(0.95105651629515357212f), s2 = kconst(0.58778525229247312917f);
     const cf t1 = v[1] + v[4], t2 = v[2] + v[3], t3 = v[1] - v[4], t4 = v[2] - v[3];
     const cf x0 = v[0];
     const cf p1 = x0 + scale(t1, c1) + scale(t2, c2);
@@ -154,7 +175,7 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     }
     __syncthreads();
     // 3. radix-8 over n1 (n = 25 n1 + n2), twiddle W200^(n2 k1); out [q][k1 * 25 + n2]
-    for (int t = tid; t < FPB * 25; t += 256) {
+    for (int t = kindex(tid); t < FPB * 25; t += 256) {
         const int q = t / 25, n2 = t - q * 25;
         cf v[8];
 #pragma unroll
@@ -165,7 +186,7 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     }
     __syncthreads();
     // 4. radix-5 over m1 (n2 = 5 m1 + m2), twiddle W25^(m2 j1) = W200^(8 m2 j1); out [q][k1*25 + m2*5 + j1]
-    for (int t = tid; t < FPB * 40; t += 256) {
+    for (int t = kindex(tid); t < FPB * 40; t += 256) {
         const int q = t / 40, r = t - q * 40, k1 = r / 5, m2 = r - k1 * 5;
         cf v[5];
 #pragma unroll
@@ -177,7 +198,7 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     }
     __syncthreads();
     // 5. radix-5 over m2 -> Z[k1 + 8 (j1 + 5 j2)] in natural order
-    for (int t = tid; t < FPB * 40; t += 256) {
+    for (int t = kindex(tid); t < FPB * 40; t += 256) {
         const int q = t / 40, r = t - q * 40, k1 = r / 5, j1 = r - k1 * 5;
         cf v[5];
 #pragma unroll
@@ -192,7 +213,7 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     //    re^2 + im^2 (the reference rounds through abs(): at most 1 ulp apart).
     float* pb = power + (int64_t)b * stridep + (int64_t)f0 * ldp;  // uniform base
     const int ldp32 = (int)ldp;
-    for (int i = tid; i < FPB * 101; i += 256) {
+    for (int i = kindex(tid); i < FPB * 101; i += 256) {
         const int q = i / 101, k = i - q * 101;
         if (f0 + q >= F) continue;
         const cf zk = zb[q][k];

@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -48,6 +48,7 @@ class GemmArgs(ctypes.Structure):
 _SIGNATURES = {
     "vasr_version": ([], ctypes.c_int),
     "vasr_set_option": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "vasr_probe_clock": ([c_p, ctypes.c_int, ctypes.c_int, c_p], ctypes.c_int),
     "vasr_last_error": ([], ctypes.c_char_p),
     "vasr_linear_x3_f32": ([ctypes.POINTER(GemmArgs), c_p, c_p], ctypes.c_int),
     "vasr_split_weights_bf16x3": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),

@@ -113,5 +113,5 @@ def graphed_step(tr) -> Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tenso
         if shard.data_ptr() != tr.audio.data_ptr():
             raise ValueError("graphed_step: scatter into the transcriber's input (shard=tr.audio)")
         tr.step()
-        return tr.tokens, tr.lengths
+        return tr.collect()  # raises if the step ran on weights changed since capture
     return step

@@ -621,6 +621,24 @@ def pooled_attention(q: torch.Tensor, kv: torch.Tensor, B: int, Lq: int, Kp: int
     return out
 
 
+def probe_clock(device, blocks: int = 2048, iters: int = 20000) -> dict:
+    """Machine state for a benchmark record (vasr_probe_clock): the shader clock over a fixed VALU
+    chain (median over workgroups, GHz) and the XCD dispatch order.  The kernels' XCD-aware block
+    maps need workgroups i and i + 8 on one XCD: round-robin dispatch, from whichever XCD the
+    dispatcher's pointer starts at (the previous launch's grid moves it: profiles/r05d/)."""
+    out = torch.zeros(3 * blocks, device=device, dtype=torch.int64)
+    check(L.lib().vasr_probe_clock(out.data_ptr(), blocks, iters, torch.cuda.current_stream(device).cuda_stream),
+          "vasr_probe_clock")
+    o = out.view(blocks, 3).cpu()
+    ghz = (o[:, 1].double() / o[:, 2].clamp(min=1).double() * 0.1).median().item()
+    xcd = o[:, 0]
+    ids = torch.arange(blocks)
+    fr = [(xcd == (ids + k) % 8).double().mean().item() for k in range(8)]
+    k = max(range(8), key=lambda j: fr[j])
+    return dict(clock_ghz=round(ghz, 3), xcd_round_robin_frac=round(fr[k], 4), xcd_start=k,
+                xcds_seen=int(xcd.unique().numel()))
+
+
 def argmax(logits: torch.Tensor) -> torch.Tensor:
     """int32 argmax over the last dim (ties -> first index)."""
     _cuda_f32("argmax.logits", logits)

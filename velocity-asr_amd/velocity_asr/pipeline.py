@@ -1,7 +1,8 @@
 """Batch transcription pipeline on the device: audio (B, S) -> tokens, no host round trip.
 
-    mel (reflect pad + DFT GEMM + log-mel)  ->  VELOCITYASR.token_ids (forward with the CTC head's
-    row argmax fused into its GEMM)  ->  CTC collapse
+    mel (real-FFT |STFT|^2 straight from the unpadded audio + log-mel; other n_fft / hop: reflect
+    pad + DFT GEMM)  ->  VELOCITYASR.token_ids (forward with the CTC head's row argmax fused into
+    its GEMM)  ->  CTC collapse
 
 Everything stays in HBM; the only device->host traffic is the (B, L) int32 token block
 and lengths when the caller asks for Python lists.  ``GraphedTranscriber`` captures the
@@ -14,7 +15,7 @@ from __future__ import annotations
 import operator
 import os
 import time
-from typing import List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 
@@ -52,6 +53,8 @@ def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0,
 
 def token_lists(toks: torch.Tensor, lens: torch.Tensor) -> List[List[int]]:
     t, n = toks.cpu().numpy(), lens.cpu().numpy()
+    if (n < 0).any() or (n > t.shape[1]).any():
+        raise ValueError("token_lists: lengths outside [0, L] (outputs of an invalidated step?)")
     return [t[b, : n[b]].tolist() for b in range(t.shape[0])]
 
 
@@ -130,10 +133,12 @@ class GraphedTranscriber:
     def _check_params(self) -> None:
         if (list(map(_VERSION, self._tensors)) != self._versions
                 or [t.data_ptr() for t in self._tensors] != self._ptrs):
-            # the replay just issued ran on the old weights: mark its outputs invalid (lengths -1,
-            # ordered after the replay on the caller's stream) so collect() cannot hand them out
+            # the replay just issued ran on the old weights: clear its outputs (zero tokens and
+            # lengths, ordered after the replay on the caller's stream) and refuse to hand them out
+            # (collect() raises); a caller holding the static buffers sees empty transcripts
             self._stale = True
-            self.lengths.fill_(-1)
+            self.tokens.zero_()
+            self.lengths.zero_()
             raise RuntimeError("GraphedTranscriber: the model's parameters changed after capture "
                                "(the graphs read the old weights); build a new GraphedTranscriber")
 
@@ -174,7 +179,9 @@ def schedule_candidates(batch: int) -> List[int]:
 
 
 def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
-                          candidates: Optional[List[int]] = None, reps: int = 5, rounds: int = 2):
+                          candidates: Optional[List[int]] = None, reps: int = 5, rounds: int = 2,
+                          audio: Optional[torch.Tensor] = None,
+                          agree: Optional[Callable[[Dict[int, float]], Dict[int, float]]] = None):
     """The GraphedTranscriber schedule that runs fastest on this device.
 
     One graph of the whole batch and two utterance-group graphs on concurrent streams give
@@ -182,10 +189,18 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
     boxes: 143.4k vs 140.4k RTFx for two groups on one, 146k vs 150k for one graph on another,
     profiles/r04r, r04t).  Each candidate is built, replayed `reps` times per round after two
     warm replays, rounds interleaved; the one with the lowest per-replay time is kept and the
-    others are released.  Returns (transcriber, {streams: best ms per replay}).  The
-    transcriber's audio holds zeros: copy the batch in before stepping."""
+    others are released.  Returns (transcriber, {streams: best ms per replay}).
+
+    audio: the (batch, samples) clips the transcriber will serve, copied into every candidate
+    before timing (the step's time depends on the data: the projection's per-chunk softplus
+    branch, exp arguments, clocks held on silence); without it the candidates time zeros.
+    agree: maps this process's {streams: ms} to the times every rank of a job decides on (e.g.
+    the max over ranks), so all ranks keep the same schedule."""
     cands = list(candidates or schedule_candidates(batch))
     trs = {s: GraphedTranscriber(model, batch, samples, device, streams=s) for s in cands}
+    if audio is not None:
+        for tr in trs.values():
+            tr.audio.copy_(audio)
     if len(cands) == 1:
         return trs[cands[0]], {}
     times = {s: float("inf") for s in cands}
@@ -199,6 +214,8 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
                 tr.step()
             torch.cuda.synchronize()
             times[s] = min(times[s], (time.perf_counter() - t0) / reps * 1e3)
+    if agree is not None:
+        times = dict(agree(times))
     best = min(cands, key=lambda s: times[s])
     keep = trs.pop(best)
     del trs  # the other graphs and their memory pools
