@@ -372,23 +372,57 @@ def run_verdict(graph_match, golden, warm_golden, golden_eager):
     return (1 if why else 0), why
 
 
-def timed(step, steps, world, dev):
+def timed(step, steps, world, dev, per_step=None):
+    """Wall time of `steps` steps between barriers + synchronizes (max over ranks).  per_step: a
+    list that receives each step's device time (ms) from HIP events recorded on the caller's
+    stream between the steps (no host synchronisation inside the loop)."""
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if per_step is not None else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    host = []
+    for i in range(steps):
+        if ev:
+            ev[i].record()
+        h0 = time.perf_counter()
         step()
+        host.append(time.perf_counter() - h0)
+    if ev:
+        ev[steps].record()
+    t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if ev:
+        per_step.extend(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
+        # host side: each step() call's own time and the loop's issue time (all steps enqueued):
+        # if they approach the device times, the host's graph launches set the pace
+        per_step.append(dict(host_step_ms=[round(v * 1e3, 4) for v in host], issue_ms=round(t_issue * 1e3, 3)))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)  # the timing group is gloo (host)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
+
+
+def step_stats(ms):
+    """Summary of the timed steps' device times (ms, HIP events between the steps on the caller's
+    stream): every step alike (a slower machine state) or a drift over the run; and the host's
+    time per step() call (graph launch + parameter check) beside it."""
+    if not ms:
+        return None
+    hostd = ms[-1] if isinstance(ms[-1], dict) else {}
+    ms = [v for v in ms if not isinstance(v, dict)]
+    v = sorted(ms)
+    hs = sorted(hostd.get("host_step_ms", []))
+    return dict(device_ms=[round(x, 4) for x in ms], min=round(v[0], 4), median=round(v[len(v) // 2], 4),
+                max=round(v[-1], 4), first_half_mean=round(float(np.mean(ms[:len(ms) // 2])), 4),
+                second_half_mean=round(float(np.mean(ms[len(ms) // 2:])), 4),
+                host_step_ms_median=round(hs[len(hs) // 2], 4) if hs else None,
+                host_step_ms_max=round(hs[-1], 4) if hs else None, host_issue_ms=hostd.get("issue_ms"))
 
 
 def run(args):
@@ -468,7 +502,10 @@ def run(args):
         if world > 1:
             dist.all_reduce(wc)
         warm_golden = golden_summary([int(v) for v in wc.tolist()], args)
-    elapsed = timed(step, args.steps, world, dev)
+    step_ms = []
+    elapsed = timed(step, args.steps, world, dev, per_step=step_ms)
+    from velocity_asr.ops import probe_clock
+    machine = probe_clock(dev)  # right after the timed steps: the clock they left, the XCD dispatch order
 
     # the tokens the timed graph wrote in its last replay vs the reference's greedy lists for the
     # same clips, and an eager pass over the same audio checked the same way (outside the timed
@@ -527,8 +564,6 @@ def run(args):
 
     rf = kernel_roofline(model, audio, args.roofline_steps, 1 if args.eager else streams)
     iso = isolated_times(model, audio[:B // (1 if args.eager else streams)])  # one utterance group's launch shape
-    from velocity_asr.ops import probe_clock
-    machine = probe_clock(dev)  # right after the isolated launches: the clock they ran at, XCD dispatch order
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -614,6 +649,7 @@ def run(args):
                    if distributed else "single process"},
         "frames_per_sec": round(frames / elapsed, 1),
         "machine": machine,
+        "step_ms_device": step_stats(step_ms),
         "roofline": roof,
         "with_scatter": scatter,
         "kernels": {
