@@ -349,8 +349,9 @@ def agree_max_over_ranks(times):
 def schedule_how(tried, world):
     if not tried:
         return "single candidate (batch under 8 clips or odd): one graph"
-    how = (f"{len(tried)} schedules built and timed on the bench's own audio in the untimed warm-up "
-           f"(5 replays x 2 rounds each); the faster kept")
+    how = (f"{len(tried)} schedules built and timed on the bench's own audio in interleaved rounds of 5 replays "
+           f"(at least 3, until each candidate's round time settles within 1 %) before the warm-up; the faster "
+           f"kept, the others freed after the timed steps")
     if world > 1:
         how += "; times are the max over ranks, so every rank keeps the same schedule"
     return how
@@ -487,25 +488,29 @@ def run(args):
             tr, tried = autotuned_transcriber(model, B, S_len, dev, audio=audio,
                                               agree=agree_max_over_ranks if world > 1 else None)
             streams = len(tr.graphs)
-            schedule = dict(chosen_streams=streams, ms_per_replay_by_streams=tried, how=schedule_how(tried, world))
+            schedule = dict(chosen_streams=streams, ms_per_replay_by_streams=tried, how=schedule_how(tried, world),
+                            rounds=tr.autotune_rounds)
         tr.audio.copy_(audio)
         step = tr.step
 
     for _ in range(args.warmup):
         step()
-    # the warm-up's last replay checked against the reference too (not only the timed leg's last)
-    warm_golden = None
-    if tr is not None:
-        torch.cuda.synchronize()
-        wt, wl = (t.clone() for t in tr.collect())
-        wc = torch.tensor(golden_check(wt, wl, args, rank), dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(wc)
-        warm_golden = golden_summary([int(v) for v in wc.tolist()], args)
+    # the warm-up's last replay is checked against the reference too, after the timed steps: its
+    # tokens are copied on the device here (no host work between the warm-up and the timed steps --
+    # an idle device starts the next steps up to 25 % slower, profiles/r05j/step_course.txt)
+    warm_copy = tuple(t.clone() for t in tr.collect()) if tr is not None else None
     step_ms = []
     elapsed = timed(step, args.steps, world, dev, per_step=step_ms)
     from velocity_asr.ops import probe_clock
     machine = probe_clock(dev)  # right after the timed steps: the clock they left, the XCD dispatch order
+    if tr is not None and hasattr(tr, "release_candidates"):
+        tr.release_candidates()  # the schedules not chosen (kept until now: freeing them stalls the device)
+    warm_golden = None
+    if warm_copy is not None:
+        wc = torch.tensor(golden_check(*warm_copy, args, rank), dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(wc)
+        warm_golden = golden_summary([int(v) for v in wc.tolist()], args)
 
     # the tokens the timed graph wrote in its last replay vs the reference's greedy lists for the
     # same clips, and an eager pass over the same audio checked the same way (outside the timed

@@ -137,6 +137,8 @@ def test_autotuned_schedule_matches_eager(model):
     tr, tried = autotuned_transcriber(model, 8, 48000, reps=2, rounds=1, audio=audio)
     assert sorted(tried) == [1, 2] and len(tr.graphs) in (1, 2)
     assert torch.equal(tr.audio, audio)  # timed on (and holding) the clips it serves
+    assert len(tr.autotune_rounds) >= 1 and all(sorted(r) == [1, 2] for r in tr.autotune_rounds)
+    tr.release_candidates()
     for _ in range(3):
         tr.step()
         assert token_lists(*tr.collect()) == exp

@@ -163,6 +163,11 @@ class GraphedTranscriber:
             main.wait_stream(st)
         self._check_params()
 
+    def release_candidates(self) -> None:
+        """Free the other schedules autotuned_transcriber built and timed beside this one."""
+        self.__dict__.pop("_candidates", None)
+        torch.cuda.synchronize(self.device)
+
     def collect(self):
         """(tokens, lengths) of the last step (the static outputs).  Raises once a step found
         the parameters changed since capture (its outputs came from the old weights)."""
@@ -179,17 +184,24 @@ def schedule_candidates(batch: int) -> List[int]:
 
 
 def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: Optional[torch.device] = None,
-                          candidates: Optional[List[int]] = None, reps: int = 5, rounds: int = 2,
+                          candidates: Optional[List[int]] = None, reps: int = 5, rounds: int = 3,
                           audio: Optional[torch.Tensor] = None,
-                          agree: Optional[Callable[[Dict[int, float]], Dict[int, float]]] = None):
+                          agree: Optional[Callable[[Dict[int, float]], Dict[int, float]]] = None,
+                          max_rounds: int = 12, settle: float = 0.01):
     """The GraphedTranscriber schedule that runs fastest on this device.
 
     One graph of the whole batch and two utterance-group graphs on concurrent streams give
     bitwise the same tokens; which is faster depends on the box (round 4, C2 on two MI355X
     boxes: 143.4k vs 140.4k RTFx for two groups on one, 146k vs 150k for one graph on another,
-    profiles/r04r, r04t).  Each candidate is built, replayed `reps` times per round after two
-    warm replays, rounds interleaved; the one with the lowest per-replay time is kept and the
-    others are released.  Returns (transcriber, {streams: best ms per replay}).
+    profiles/r04r, r04t).  Each candidate is built, then replayed in interleaved rounds (two warm
+    replays, then `reps` timed); rounds continue past `rounds` until every candidate's last round
+    is within `settle` of its previous one (at most `max_rounds`): a device fresh from idle runs
+    the same replays up to 25 % slower for its first few tens of milliseconds of load
+    (profiles/r05h/), so early rounds would time the ramp, not the schedule.  The fastest
+    candidate is returned; the others are kept alive on it until release_candidates() (freeing a
+    graph's memory pool stalls the device, which would idle it between the tuning and the caller's
+    first steps).  Returns (transcriber, {streams: best ms per replay}); the transcriber's
+    .autotune_rounds holds every round's times.
 
     audio: the (batch, samples) clips the transcriber will serve, copied into every candidate
     before timing (the step's time depends on the data: the projection's per-chunk softplus
@@ -202,9 +214,13 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
         for tr in trs.values():
             tr.audio.copy_(audio)
     if len(cands) == 1:
-        return trs[cands[0]], {}
+        tr = trs[cands[0]]
+        tr.autotune_rounds = []
+        return tr, {}
     times = {s: float("inf") for s in cands}
-    for _ in range(rounds):
+    hist: List[Dict[int, float]] = []
+    for r in range(max_rounds):
+        this = {}
         for s, tr in trs.items():
             tr.step()
             tr.step()
@@ -213,12 +229,16 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
             for _ in range(reps):
                 tr.step()
             torch.cuda.synchronize()
-            times[s] = min(times[s], (time.perf_counter() - t0) / reps * 1e3)
+            this[s] = (time.perf_counter() - t0) / reps * 1e3
+            times[s] = min(times[s], this[s])
+        hist.append(this)
+        if r + 1 >= rounds and (len(hist) < 2 or all(abs(hist[-1][s] - hist[-2][s]) <= settle * hist[-1][s]
+                                                      for s in cands)):
+            break
     if agree is not None:
         times = dict(agree(times))
     best = min(cands, key=lambda s: times[s])
     keep = trs.pop(best)
-    del trs  # the other graphs and their memory pools
-    torch.cuda.synchronize()
+    keep._candidates = list(trs.values())  # released by release_candidates()
+    keep.autotune_rounds = [{s: round(t, 4) for s, t in h.items()} for h in hist]
     return keep, {s: round(t, 4) for s, t in times.items()}
-
