@@ -1,0 +1,11 @@
+#!/bin/bash
+# r05r: scan with wave-priority rotation between the three blocks of a CU (time-based phases of 2^12/13/15
+# cycles, or chunk-index phases) vs without, B=32 and B=16, mode 2.
+set -uo pipefail
+O=gpurun_out/r05r
+mkdir -p $O
+export TMPDIR=/tmp
+for b in 32 16 8; do
+SCAN_MODES=2 SCAN_B=$b VARIANT_DIR=_abl8 timeout -k 10 300 python -u tools/scan_ablate_run.py > $O/b$b.txt 2>&1 || { echo "b$b rc $?"; tail -5 $O/b$b.txt; exit 1; }
+cat $O/b$b.txt
+done

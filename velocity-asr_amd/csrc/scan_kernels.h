@@ -40,6 +40,12 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+#ifdef VASR_SCAN_STAMPS
+// Diagnostic builds only (tools/diag/scan_clock.py): per workgroup of the streaming kernel {XCC id,
+// s_memtime and s_memrealtime at entry and exit} -- the shader clock the launch ran at.
+__device__ int64_t* g_scan_stamps;
+#endif
+
 #ifndef VASR_SCAN_ABLATE
 #define VASR_SCAN_ABLATE 0  // diagnostic builds only (tools/scan_ablate.sh): 1 no exp,
 #endif                      // 4 no B/C LDS reads, 8 no chunk staging after the first,
@@ -55,6 +61,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 #endif
 #ifndef VASR_SCAN_FASTSTAGE
 #define VASR_SCAN_FASTSTAGE 1  // 0: every chunk's staging addresses from the clamped index path
+#endif
+#ifndef VASR_SCAN_PRIO
+#define VASR_SCAN_PRIO 0  // wave priority rotation between the blocks sharing a CU (see ssm_scan_kernel)
+#endif
+#ifndef VASR_SCAN_PRIO_SHIFT
+#define VASR_SCAN_PRIO_SHIFT 13  // rotation period: 2^SHIFT shader cycles per priority phase
 #endif
 #ifndef VASR_SCAN_PACKED
 #define VASR_SCAN_PACKED 1  // 1: state pairs as float2 vectors (v_pk_*_f32); 0: scalar pairs

@@ -36,3 +36,9 @@ int scan_chunked_n64(bool two, int mode, const float* xz, int64_t ld_xz, const f
                      : chunked<2>(two, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, ws_a, ws_b, s);
 }
 }  // namespace vasr
+
+#ifdef VASR_SCAN_STAMPS
+VASR_API int vasr_diag_scan_stamps(void* buf) {  // diagnostic builds only (N = 64 kernels)
+    return hipMemcpyToSymbol(HIP_SYMBOL(vasr::g_scan_stamps), &buf, sizeof(buf)) == hipSuccess ? VASR_OK : VASR_EINVAL;
+}
+#endif
