@@ -23,15 +23,22 @@ def main():
     out = torch.empty(M, Di, device="cuda")
     libs = sorted(glob.glob(os.path.join(HERE, os.environ.get("VARIANT_DIR", "_variants"), "lib_*.so")), key=lambda p: int(os.path.basename(p).split("_")[1]))
     fns = []
+    chunked = os.environ.get("SCAN_FORM", "streaming") == "chunked"  # the chunk-parallel form (3 launches)
+    wsf = 4 * B * ((L + 15) // 16) * Di * N
+    ws = torch.empty(wsf, device="cuda")
     for p in libs:
         lib = ctypes.CDLL(p)
-        f = lib.vasr_ssm_scan_f32
         c_p, c_i64 = ctypes.c_void_p, ctypes.c_int64
-        f.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p]
+        if chunked:
+            f = lib.vasr_ssm_scan_chunked_f32
+            f.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p, c_i64, c_p]
+        else:
+            f = lib.vasr_ssm_scan_f32
+            f.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p]
         fns.append((os.path.basename(p), f))
     st = torch.cuda.current_stream().cuda_stream
     args = lambda mode: (xz.data_ptr(), 2 * Di, dt.data_ptr(), Di, bc.data_ptr(), 2 * N, A2.data_ptr(), D.data_ptr(),
-                         out.data_ptr(), Di, B, L, Di, N, mode, st)
+                         out.data_ptr(), Di, B, L, Di, N, mode) + ((ws.data_ptr(), wsf, st) if chunked else (st,))
     res = {}
     for rnd in range(5):
         for n, f in fns:
