@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def main():
-    B, L, Di, N = int(os.environ.get("SCAN_B", 32)), 501, 384, 64
+    B, L, Di, N = int(os.environ.get("SCAN_B", 32)), int(os.environ.get("SCAN_L", 501)), 384, 64
     modes = tuple(int(m) for m in os.environ.get("SCAN_MODES", "0").split(","))
     M = B * L
     g = torch.Generator(device="cuda").manual_seed(0)

@@ -33,6 +33,8 @@
 // an XCD (its 4 MiB L2 then serves the B/C slices and the 64-B row segments they share).
 #pragma once
 
+#include <type_traits>
+
 #include "vasr_internal.h"
 
 namespace vasr {
