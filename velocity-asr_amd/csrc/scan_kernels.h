@@ -71,6 +71,9 @@ __device__ int64_t* g_scan_stamps;
 #ifndef VASR_SCAN_PRIO_SHIFT
 #define VASR_SCAN_PRIO_SHIFT 13  // rotation period: 2^SHIFT shader cycles per priority phase
 #endif
+#ifndef VASR_SCAN_UPPER_REG
+#define VASR_SCAN_UPPER_REG 5  // upper-stack levels held in registers (the rest in LDS)
+#endif
 #ifndef VASR_SCAN_PACKED
 #define VASR_SCAN_PACKED 1  // 1: state pairs as float2 vectors (v_pk_*_f32); 0: scalar pairs
 #endif
