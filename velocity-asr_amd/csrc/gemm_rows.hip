@@ -335,12 +335,25 @@ template <int KS>
 int launch_rows(const GemmParams& p, int epi, hipStream_t s) {
     const int NT = (p.N + 31) / 32;
     const int row_blocks = (p.M + 32 * RW - 1) / (32 * RW);
-    // column groups: at most one block per CU (LDS: NSLOT x 36 KiB per block), so the grid is a
-    // single round -- a second, partial round costs as much as the first
-    int groups = row_blocks >= kCUs ? 1 : kCUs / row_blocks;
-    groups = max(1, min(groups, NT));
-    const int per = min((NT + groups - 1) / groups, MAX_GROUP);
-    groups = (NT + per - 1) / per;
+    // column groups: at most one block per CU (LDS: NSLOT x 36 KiB per block), so a grid of more
+    // than kCUs blocks runs in rounds, and a partial round costs as much as a full one.  The
+    // groups minimise rounds x (chunks per block + 1), the 1 standing for a block's A prologue
+    // (its 256 rows loaded and split): M = 16032 keeps 4 groups of 10 chunks (252 blocks, one
+    // round); the 30-s clips' M = 48096 takes 4 groups in 3 rounds (30 chunk-steps per CU) instead
+    // of 3 groups of 16 (the MAX_GROUP cap) in 3 rounds (48), M = 24048 5 groups of 8 in 2 rounds
+    // (16) instead of 3 of 16 in 2 (32).
+    int groups = 1, per = min(NT, MAX_GROUP), best = -1;
+    for (int g = 1; g <= NT; ++g) {
+        const int pg = (NT + g - 1) / g;
+        if (pg > MAX_GROUP) continue;
+        const int gg = (NT + pg - 1) / pg;
+        const int cost = ((row_blocks * gg + kCUs - 1) / kCUs) * (pg + 1);
+        if (best < 0 || cost < best) {
+            best = cost;
+            groups = gg;
+            per = pg;
+        }
+    }
     const dim3 grid(row_blocks * groups), block(64 * RW);
 #define VASR_R(E) hipLaunchKernelGGL((gemm_rows_kernel<KS, E>), grid, block, 0, s, p, groups, per)
     switch (epi) {
