@@ -1,0 +1,19 @@
+#!/bin/bash
+# r05af: round-5 evidence at HEAD: GPU suite, smoke, two default bench lines, the config lines, and the
+# rocprofv3 kernel trace + FETCH/WRITE passes of the default bench command.
+set -uo pipefail
+O=gpurun_out/r05af
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?
+tail -2 $O/gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke rc $?"; tail -5 $O/smoke.txt; exit 1; }
+echo smoke ok
+for i in 1 2; do
+timeout -k 10 300 python -u bench.py > $O/bench$i.json 2> $O/bench$i.err || { echo "bench rc $?"; tail -5 $O/bench$i.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench$i.json')); s=d['config']['schedule']; print('c2', d['value'], d['ms_per_step'], s['chosen_streams'], s['ms_per_replay_by_streams'], d['roofline']['avg_launch_us'], d['roofline']['frac'], d['cpu_baseline']['value'] if d.get('cpu_baseline') else None, d['machine']['clock_ghz'])"
+done
+timeout -k 10 1500 bash tools/config_benches.sh r05af || { echo "configs rc $?"; exit 1; }
+for f in gpurun_out/cfg_r05af/*.json; do python3 -c "import json; d=json.load(open('$f')); s=d['config'].get('schedule') or {}; print('$(basename $f .json)', d['value'], d['ms_per_step'], s.get('chosen_streams'), s.get('ms_per_replay_by_streams'), d['roofline']['avg_launch_us'], d['tokens_vs_reference']['all_ranks_pass'] if d.get('tokens_vs_reference') else None, d['machine']['clock_ghz'])"; done
+timeout -k 10 1000 bash tools/profile.sh r05af || { echo "profile rc $?"; exit 1; }
+echo profile done
