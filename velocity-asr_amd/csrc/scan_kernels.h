@@ -66,7 +66,8 @@ __device__ int64_t* g_scan_stamps;
 #endif
 #ifndef VASR_SCAN_PRIO
 #define VASR_SCAN_PRIO 4  // wave priority between the blocks sharing a CU (ssm_scan_kernel): 0 off, 1 time
-                          // phases, 2 chunk-index rotation, 3 fewer chunks first, 4 = 3 at >= 3 blocks per CU else 2
+                          // phases, 2 chunk-index rotation, 3 fewer chunks first (quarters), 5 = 3 with the last
+                          // quarter by youth, 4 = 5 at >= 3 blocks per CU else 2
 #endif
 #ifndef VASR_SCAN_PRIO_SHIFT
 #define VASR_SCAN_PRIO_SHIFT 13  // rotation period: 2^SHIFT shader cycles per priority phase
