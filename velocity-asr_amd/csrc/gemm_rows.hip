@@ -103,41 +103,10 @@ __device__ unsigned long long* g_rows_stamps;
 // which the hardware drops), so the kernel's counted vmcnt waits stay exact.  No vector-memory
 // loads besides the residual / positional operand, so the compiler's own vmcnt waits for those
 // are the only ones that also cover the LDS-DMA ring in flight.
-// WIDE (N a multiple of 32, C rows 16-B aligned): each 4 x 4 block of a lane quad (4 columns x
-// 4 rows of the accumulator) is transposed in registers (two DPP exchange stages) so that a lane
-// holds 4 consecutive columns of one row, and a chunk leaves as 4 buffer_store_dwordx4 (8 rows x
-// 128 B each) instead of 16 dword stores (2 rows x 128 B); the stored values are the same.
-#ifndef VASR_ROWS_WIDE
-#define VASR_ROWS_WIDE 1
-#endif
-template <bool WIDE>
-constexpr int nst() { return WIDE ? 4 : 16; }  // store instructions per wave per chunk
+constexpr int NST = 16;  // store instructions per wave per chunk
 constexpr int OOB = 0x7FFFFFFC;
 
-// lane t of each quad reads lane t ^ 2 (CTRL 0x4E) or t ^ 1 (0xB1)
-template <int CTRL>
-__device__ __forceinline__ float quad_xchg(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-
-// e[i] = (row R + i, column c0 + t) in lane t of a quad -> e[i] = (row R + t, column c0 + i)
-__device__ __forceinline__ void quad_transpose(float (&e)[4], int lane) {
-    const bool b1 = lane & 2, b0 = lane & 1;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const float u = quad_xchg<0x4E>(b1 ? e[k] : e[k + 2]);
-        if (b1) e[k] = u;
-        else e[k + 2] = u;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k += 2) {
-        const float u = quad_xchg<0xB1>(b0 ? e[k] : e[k + 1]);
-        if (b0) e[k] = u;
-        else e[k + 1] = u;
-    }
-}
-
-template <int EPI, bool WIDE = false>
+template <int EPI>
 __device__ __forceinline__ void rows_epilogue(const GemmParams& p, __amdgpu_buffer_rsrc_t cbuf, int m0, int n0,
                                               const floatx16& acc, int r, int h, const float* __restrict__ bias_s,
                                               const float4* __restrict__ qp_s, int cfirst) {
@@ -170,38 +139,6 @@ __device__ __forceinline__ void rows_epilogue(const GemmParams& p, __amdgpu_buff
     auto body = [&](auto SPc) {
         constexpr int SP = decltype(SPc)::value;
         const bool sp = SP == 1 || (SP == 2 && col >= p.n_out);
-        if constexpr (WIDE) {
-            static_assert(EPI == VASR_EPI_NONE || EPI == VASR_EPI_GELU || EPI == VASR_EPI_SOFTPLUS_FROM,
-                          "wide stores: column-only epilogues");
-            float v[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float x = acc[i];
-                if (p.bias) x = x + bv;
-                if (p.qp) x = fake_quant(x, qc);
-                if constexpr (EPI == VASR_EPI_GELU) {
-                    x = gelu_fast(x);
-                } else if constexpr (EPI == VASR_EPI_SOFTPLUS_FROM) {
-                    if constexpr (SP == 1) x = softplus20_fast(x);
-                    else if constexpr (SP == 2) x = sp ? softplus20_fast(x) : x;
-                }
-                v[i] = x;
-            }
-            const int t = r & 3, cq = n0 + (r & ~3);  // this lane's row in a 4-row group, its 4 columns
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float e[4] = {v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
-                quad_transpose(e, r);
-                const int row = m0 + 8 * j + 4 * h + t;
-                typedef float f32x4 __attribute__((ext_vector_type(4)));
-                const f32x4 q4 = {e[0], e[1], e[2], e[3]};
-                if (!(VASR_ROWS_ABLATE & 2))
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, q4),
-                                                           cbuf, row < p.M ? (row * (int)p.ldc + cq) * 4 : OOB, 0,
-                                                           VASR_ROWS_STORE_AUX);
-            }
-            return;
-        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int row = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -235,7 +172,7 @@ __device__ __forceinline__ void rows_epilogue(const GemmParams& p, __amdgpu_buff
     }
 }
 
-template <int KS, int EPI, bool WIDE = false>
+template <int KS, int EPI>
 __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int n_groups, int chunks_per_group) {
     constexpr int CHUNK = KS * 3 * 1024;       // one 32-column W chunk: [KS][3 planes][64 lanes][16 B]
     constexpr int DW = 4;                      // loader waves (the first four) issue the chunk's DMA
@@ -327,7 +264,7 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         // (one event type: in order): they keep the stores of steps j - DEPTH + 1 .. j - 1 in
         // flight and bound the older ones.
         int n_vm = 0;
-        if (!loader && !(VASR_ROWS_ABLATE & 2)) n_vm = VASR_ROWS_STORE_WAIT ? nst<WIDE>() * max(0, j - max(j - DEPTH + 1, 1)) : 63;
+        if (!loader && !(VASR_ROWS_ABLATE & 2)) n_vm = VASR_ROWS_STORE_WAIT ? NST * max(0, j - max(j - DEPTH + 1, 1)) : 63;
         VASR_STAMP(t0);
         wait_vmcnt_rt(min(n_vm, 63));
         VASR_STAMP(t1);
@@ -338,7 +275,7 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         bf16x8 wf[2][3];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) wf[0][pl] = *reinterpret_cast<const bf16x8*>(wb + pl * 1024);
-        if (j >= 1) rows_epilogue<EPI, WIDE>(p, cbuf, m0, (c0 + j - 1) * 32, acc[S ^ 1], r, h, bias_s, qp_s, cfirst);
+        if (j >= 1) rows_epilogue<EPI>(p, cbuf, m0, (c0 + j - 1) * 32, acc[S ^ 1], r, h, bias_s, qp_s, cfirst);
         VASR_STAMP(t3);
         if (j + DEPTH < nc && !(VASR_ROWS_ABLATE & 4)) issue(j + DEPTH);
         VASR_STAMP(t4);
@@ -382,7 +319,7 @@ __global__ __launch_bounds__(64 * RW, 1) void gemm_rows_kernel(GemmParams p, int
         if (j + 1 < nc) step(std::integral_constant<int, 1>(), j + 1);
     }
     const int jl = nc - 1;  // the last chunk's epilogue
-    rows_epilogue<EPI, WIDE>(p, cbuf, m0, (c0 + jl) * 32, (jl & 1) ? acc[1] : acc[0], r, h, bias_s, qp_s, cfirst);
+    rows_epilogue<EPI>(p, cbuf, m0, (c0 + jl) * 32, (jl & 1) ? acc[1] : acc[0], r, h, bias_s, qp_s, cfirst);
 #ifdef VASR_ROWS_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     VASR_STAMP(st_end);
@@ -419,20 +356,16 @@ int launch_rows(const GemmParams& p, int epi, hipStream_t s) {
     }
     const dim3 grid(row_blocks * groups), block(64 * RW);
 #define VASR_R(E) hipLaunchKernelGGL((gemm_rows_kernel<KS, E>), grid, block, 0, s, p, groups, per)
-#define VASR_RW(E) hipLaunchKernelGGL((gemm_rows_kernel<KS, E, true>), grid, block, 0, s, p, groups, per)
-    // wide stores: every chunk full (N a multiple of 32) and C rows 16-B aligned
-    const bool wide = VASR_ROWS_WIDE && p.N % 32 == 0 && p.ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(p.C) & 15) == 0;
     switch (epi) {
-        case VASR_EPI_NONE: if (wide) VASR_RW(VASR_EPI_NONE); else VASR_R(VASR_EPI_NONE); break;
-        case VASR_EPI_GELU: if (wide) VASR_RW(VASR_EPI_GELU); else VASR_R(VASR_EPI_GELU); break;
-        case VASR_EPI_SOFTPLUS_FROM: if (wide) VASR_RW(VASR_EPI_SOFTPLUS_FROM); else VASR_R(VASR_EPI_SOFTPLUS_FROM); break;
+        case VASR_EPI_NONE: VASR_R(VASR_EPI_NONE); break;
+        case VASR_EPI_GELU: VASR_R(VASR_EPI_GELU); break;
+        case VASR_EPI_SOFTPLUS_FROM: VASR_R(VASR_EPI_SOFTPLUS_FROM); break;
         case VASR_EPI_RESIDUAL: VASR_R(VASR_EPI_RESIDUAL); break;
         case VASR_EPI_GELU_PE: VASR_R(VASR_EPI_GELU_PE); break;
         case VASR_EPI_ARGMAX: VASR_R(VASR_EPI_ARGMAX); break;
         default: set_error("vasr_linear_x3_f32: rows engine: epilogue %d not supported", epi); return VASR_EINVAL;
     }
 #undef VASR_R
-#undef VASR_RW
     return launch_status("vasr_linear_x3_f32");
 }
 
