@@ -69,6 +69,9 @@ __device__ int64_t* g_scan_stamps;
                           // phases, 2 chunk-index rotation, 3 fewer chunks first (quarters), 5 = 3 with the last
                           // quarter by youth, 4 = 5 at >= 3 blocks per CU else 2
 #endif
+#ifndef VASR_SCAN_PRIO_ROT
+#define VASR_SCAN_PRIO_ROT 3  // priorities 0 .. ROT-1 rotated by chunk index where fewer than 3 blocks share a CU
+#endif
 #ifndef VASR_SCAN_PRIO_SHIFT
 #define VASR_SCAN_PRIO_SHIFT 13  // rotation period: 2^SHIFT shader cycles per priority phase
 #endif
