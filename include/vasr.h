@@ -51,7 +51,9 @@ enum vasr_option {
     VASR_OPT_TAIL_ROWS = 2,  /* token rows per fused-SSMBlock-tail workgroup: 0, 16, 32 (VASR_TAIL_ROWS)   */
     VASR_OPT_GEMM_ENGINE = 3, /* split-bf16 GEMM main loop: 0 auto, 1 LDS-ring tiles, 2 A-rows-stationary
                                  (K = 128 / 192, batch 1, unpaired epilogues) (VASR_GEMM_ENGINE)         */
-    VASR_OPT_TAIL_WAVES = 4   /* waves per fused-SSMBlock-tail workgroup: 0, 4, 6, 12 (VASR_TAIL_WAVES)    */
+    VASR_OPT_TAIL_WAVES = 4,  /* waves per fused-SSMBlock-tail workgroup: 0, 4, 6, 12 (VASR_TAIL_WAVES)    */
+    VASR_OPT_SCAN_SPLIT = 5   /* form of vasr_ssm_scan_chunked_f32: 0 auto, 1 three launches, 2 one launch
+                                 (time split inside the workgroup) (VASR_SCAN_SPLIT)                     */
 };
 int vasr_set_option(int key, int value);
 
@@ -186,8 +188,11 @@ int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t l
  * streaming kernel's 16-step chunks; pass 1 forms each chunk's up-sweep composite, pass 2
  * the composites of aligned blocks of 2^k chunks (the entries of the streaming kernel's
  * chunk-level stack), pass 3 folds each chunk's prefix from them and runs the chunk's tree
- * with the y reduction and gate.  Same float
- * operations as vasr_ssm_scan_f32 with the same lane layout: bitwise equal outputs.
+ * with the y reduction and gate.  Launches whose workgroups fit the CUs once (N <= 64, B * Di * N
+ * / 128 <= 256; VASR_OPT_SCAN_SPLIT) run the same passes in ONE launch instead: a workgroup
+ * owns one wave's channels and its waves split time into ranges of aligned 8-step chunk blocks
+ * (2 state indices per lane; the workspace is then unused).  Same float operations as
+ * vasr_ssm_scan_f32 with the same lane layout: bitwise equal outputs.
  * workspace: >= vasr_ssm_scan_workspace_floats(B, L, Di, N) floats, 16-byte aligned. */
 int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,
                               const float* bc, int64_t ld_bc, const float* A2, const float* D,

@@ -85,14 +85,18 @@ def test_chunked_state_dims_and_model_width(tc, N, Di):
 
 @pytest.mark.gpu
 def test_chunked_is_the_default_for_one_utterance():
-    """The model shape at B = 1 takes the chunked form; at the bench's 16-clip launches, at
-    B = 4 (384 waves) and for the global blocks' short L the streaming kernel (profiles/r03ae)."""
-    from velocity_asr import ops
+    """The model shape at B = 1 takes the chunked form, and so do the global blocks' short L
+    at B = 1 (one launch: the time-split form, profiles/r05aq); at the bench's 16-clip launches
+    and at B = 4 (384 waves) the streaming kernel (profiles/r03ae)."""
+    from velocity_asr import _lib, ops
     assert ops._use_chunked(1, 501, 384, 64, 2) and ops._use_chunked(2, 1501, 384, 64, 0)
     assert ops._use_chunked(1, 187, 384, 32, 2)
     assert not ops._use_chunked(16, 501, 384, 64, 2)
     assert not ops._use_chunked(4, 501, 384, 64, 2)
-    assert not ops._use_chunked(1, 64, 384, 32, 2)   # the global blocks at 10 s
+    assert ops._use_chunked(1, 64, 384, 32, 2)   # the global blocks at 10 s: one launch
+    with ops.option(_lib.OPT_SCAN_SPLIT, 1):
+        assert not ops._use_chunked(1, 64, 384, 32, 2)   # three launches: streaming wins at L = 64
+    assert not ops._use_chunked(32, 64, 384, 32, 2)
     assert not ops._use_chunked(1, 501, 384, 64, 1)  # the recurrence keeps its own kernel
     assert not ops._use_chunked(1, 16, 384, 64, 2)   # one chunk: nothing to parallelise
 
@@ -115,6 +119,86 @@ def test_one_utterance_30s_tokens_match_reference():
         ls = _form("streaming", m, mel)
     assert torch.equal(lc, ls)
     np.testing.assert_array_equal(lc.argmax(-1).cpu().numpy(), golden("fwd_b1_30s.npz")["tokens"])
+
+
+def _run_split(x, dt, Bm, Cm, A_log, D, z, mode, split):
+    """vasr_ssm_scan_chunked_f32 through the C ABI with VASR_OPT_SCAN_SPLIT = split (1: three
+    launches, 2: one launch) at 2 state indices per lane (any L, also L <= 16)."""
+    from velocity_asr import _lib, ops
+    B, L, Di = x.shape
+    N = Bm.shape[-1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    xz = t(np.concatenate([x.reshape(B * L, Di), z.reshape(B * L, Di)], 1))
+    bc = t(np.concatenate([Bm.reshape(B * L, N), Cm.reshape(B * L, N)], 1))
+    dtt = t(dt.reshape(B * L, Di))
+    A2 = t(((-np.exp(A_log)).astype(np.float32) * np.float32(1.4426950408889634)).astype(np.float32))
+    Dt = t(D)
+    out = torch.full((B * L, Di), float("nan"), device=DEV)
+    lib = _lib.load()
+    ws = torch.empty(max(1, int(lib.vasr_ssm_scan_workspace_floats(B, L, Di, N))), device=DEV)
+    with ops.option(_lib.OPT_SCAN_LANES, 2), ops.option(_lib.OPT_SCAN_SPLIT, split):
+        rc = lib.vasr_ssm_scan_chunked_f32(xz.data_ptr(), 2 * Di, dtt.data_ptr(), Di, bc.data_ptr(), 2 * N,
+                                           A2.data_ptr(), Dt.data_ptr(), out.data_ptr(), Di, B, L, Di, N, mode,
+                                           ws.data_ptr(), ws.numel(), None)
+        assert rc == 0, lib.vasr_last_error()
+        torch.cuda.synchronize()
+    return out.cpu().numpy().reshape(B, L, Di)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("B,L", [(1, 1), (1, 7), (1, 8), (1, 9), (1, 16), (1, 17), (3, 100), (1, 128), (1, 129),
+                                 (1, 257), (1, 501), (2, 501), (1, 1024), (1, 1025), (1, 1501), (1, 4100), (1, 8192)])
+def test_split_bitwise_equals_streaming(mode, B, L):
+    """The one-launch time-split form (phase-1 range composites, the segment tree over the
+    waves, each range's streaming tree from its folded prefix) equals the streaming kernel of
+    the same lane layout and the three-launch form bit for bit: ranges of 1 .. 64 chunks of 8
+    steps (L up to 8192), a ragged last chunk, one-chunk launches, several utterances."""
+    from velocity_asr import _lib, ops
+    args = _inputs(17 * L + B, B, L, 64, 64)
+    with ops.option(_lib.OPT_SCAN_LANES, 2):
+        stream = _form("streaming", _run, *args, mode)
+    one = _run_split(*args, mode, 2)
+    np.testing.assert_array_equal(one, stream)
+    if L > 16:
+        np.testing.assert_array_equal(_run_split(*args, mode, 1), stream)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,Di,L", [(16, 64, 300), (32, 384, 187), (32, 384, 501), (64, 384, 501), (64, 384, 1501)])
+def test_split_state_dims_and_model_width(N, Di, L):
+    """The model's shapes (local blocks N = 64, Di = 384; global blocks N = 32) and N = 16."""
+    from velocity_asr import _lib, ops
+    args = _inputs(5 * N + L, 1, L, Di, N)
+    with ops.option(_lib.OPT_SCAN_LANES, 2):
+        stream = _form("streaming", _run, *args, 2)
+    np.testing.assert_array_equal(_run_split(*args, 2, 2), stream)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["b1_30s", "b2_10s_first"])
+def test_one_utterance_split_form_tokens_match_reference(case):
+    """One utterance through the one-launch scan (the default at B = 1): argmax tokens equal the
+    reference goldens (30 s; the first 10-s clip of fwd_b2_10s on its own) and the logits equal
+    the streaming form's (2 states per lane) bit for bit."""
+    import velocity_asr as va
+    from conftest import golden
+    from velocity_asr import synthetic as S
+    from velocity_asr import _lib, ops
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    if case == "b1_30s":
+        audio, tokens = S.make_audio(1, 480000, seed=4321), golden("fwd_b1_30s.npz")["tokens"]
+    else:
+        audio, tokens = S.make_audio(2, 160000, seed=1234)[:1], golden("fwd_b2_10s.npz")["tokens"][:1]
+    mel = va.compute_mel_spectrogram(torch.from_numpy(np.ascontiguousarray(audio)).to(DEV))
+    with ops.option(_lib.OPT_SCAN_LANES, 2):
+        lc = _form("chunked", m, mel)
+        ls = _form("streaming", m, mel)
+    assert torch.equal(lc, ls)
+    np.testing.assert_array_equal(lc.argmax(-1).cpu().numpy(), tokens)
 
 
 def test_chunked_workspace_size():

@@ -75,6 +75,23 @@ VASR_API int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const flo
     float* ws_a = workspace;
     float* ws_b = workspace + need / 2;
     hipStream_t s = as_stream(stream);
+    // Form: one launch (time split inside a workgroup of one wave's channels, 2 state indices per
+    // lane, N <= 64) while its B * Di / DPW workgroups fit the CUs once (~157 KiB of LDS each) and
+    // L <= 512, else the three launches below.  The one launch is VALU-bound on B * Di * N / 128
+    // CUs (192 at the model's B = 1): 16.2-16.8 vs 18 us for the three launches at L = 501, but
+    // slower from L ~ 1000 (one-utterance 30 s: 0.806 vs 0.777 ms; profiles/r05ap).
+    // vasr_set_option(VASR_OPT_SCAN_SPLIT, 1|2) (env VASR_SCAN_SPLIT) forces them (three | one).
+    // A forced 4-states-per-lane layout takes the three launches.
+    const int split_opt = option(VASR_OPT_SCAN_SPLIT);
+    const bool split_ok = N <= 64 && option(VASR_OPT_SCAN_LANES) != 4;
+    if (split_ok && (split_opt == 2 || (split_opt == 0 && (int64_t)B * Di * N / 128 <= 256 && L <= 512))) {
+        switch (N) {
+            case 16: return scan_split_n16(mode, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
+            case 32: return scan_split_n32(mode, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
+            case 64: return scan_split_n64(mode, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
+            default: break;  // other N: the three launches report it
+        }
+    }
     // lane layout: 4 state indices per lane (the chunk-parallel grid has waves enough; 2 per lane
     // measured slower: 40.0 vs 35.9 us at B = 1, L = 501 and 43.4 vs 37.7 at L = 1501);
     // VASR_OPT_SCAN_LANES = 2 forces the other (outputs are bitwise those of the streaming kernel with

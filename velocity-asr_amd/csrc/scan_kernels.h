@@ -295,4 +295,13 @@ VASR_SCAN_LAUNCHERS(32)
 VASR_SCAN_LAUNCHERS(64)
 VASR_SCAN_LAUNCHERS(128)
 #undef VASR_SCAN_LAUNCHERS
+// One-launch time-split form (2 state indices per lane; N <= 64)
+#define VASR_SCAN_SPLIT_LAUNCHER(NN)                                                                               \
+    int scan_split_n##NN(int mode, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt, const float* bc, \
+                         int64_t ld_bc, const float* A2, const float* D, float* out, int64_t ld_out, int B, int L,   \
+                         int Di, hipStream_t s);
+VASR_SCAN_SPLIT_LAUNCHER(16)
+VASR_SCAN_SPLIT_LAUNCHER(32)
+VASR_SCAN_SPLIT_LAUNCHER(64)
+#undef VASR_SCAN_SPLIT_LAUNCHER
 }  // namespace vasr

@@ -35,4 +35,11 @@ int scan_chunked_n32(bool two, int mode, const float* xz, int64_t ld_xz, const f
     return mode == 0 ? chunked<0>(two, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, ws_a, ws_b, s)
                      : chunked<2>(two, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, ws_a, ws_b, s);
 }
+
+int scan_split_n32(int mode, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt, const float* bc,
+                    int64_t ld_bc, const float* A2, const float* D, float* out, int64_t ld_out, int B, int L, int Di,
+                    hipStream_t s) {
+    return mode == 0 ? npl2::launch_split_n<N, 0>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
+                     : npl2::launch_split_n<N, 2>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
+}
 }  // namespace vasr

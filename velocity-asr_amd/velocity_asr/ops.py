@@ -408,9 +408,14 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
 # 37.0 at N = 64) and lose at 384 (B = 4, N = 64: 41.9 vs 39.1) and for short L (the global
 # blocks' L = 64 at 10 s: 10.2 vs 6.8 us).
 # scan_form("streaming" | "chunked" | None) forces one (default from VASR_SCAN_CHUNKED=0|1).
+# Below CHUNKED_MIN_L the chunked entry point still wins where it runs as ONE launch (the
+# time-split form: N <= 64, B * Di * N / 128 <= 256 workgroups, L <= 512; include/vasr.h), e.g.
+# the global blocks' L = 64 at B = 1 (VASR_SCAN_SPLIT_SHORT=0 turns this off; profiles/r05aq).
 CHUNKED_MAX_WAVES = 256
 CHUNKED_MIN_L = 160
+SPLIT_MAX_L = 512
 _SCAN_FORM = {"0": "streaming", "1": "chunked"}.get(os.environ.get("VASR_SCAN_CHUNKED", ""))
+_SPLIT_SHORT = os.environ.get("VASR_SCAN_SPLIT_SHORT", "1") != "0"
 
 
 def scan_form(form: Optional[str]) -> Optional[str]:
@@ -428,7 +433,16 @@ def _use_chunked(B: int, Lq: int, Di: int, N: int, mode: int) -> bool:
         return False
     if _SCAN_FORM is not None:
         return _SCAN_FORM == "chunked"
+    if _SPLIT_SHORT and _split_form(B, Lq, Di, N):
+        return True
     return B * Di * N // 256 < CHUNKED_MAX_WAVES and Lq > CHUNKED_MIN_L
+
+
+def _split_form(B: int, Lq: int, Di: int, N: int) -> bool:
+    """vasr_ssm_scan_chunked_f32 runs this launch as one (the time-split form) under the default
+    options (scan.hip's rule)."""
+    return (N <= 64 and B * Di * N // 128 <= 256 and Lq <= SPLIT_MAX_L
+            and L.lib().vasr_set_option(L.OPT_SCAN_SPLIT, -1) != 1 and L.lib().vasr_set_option(L.OPT_SCAN_LANES, -1) != 4)
 
 
 SCAN_STATE_DIMS = (16, 32, 64, 128)  # the scan kernels' state dims (include/vasr.h)
