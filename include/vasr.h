@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 13
+#define VASR_ABI_VERSION 14
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -371,6 +371,14 @@ int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse
 int vasr_ctc_collapse_var(const int32_t* pred, int B, int L, const int32_t* frames, int blank, int collapse,
                           int32_t* out_tokens, int32_t* out_len, int32_t* out_start, int32_t* out_end,
                           void* stream);
+/* Greedy decode straight from a VASR_EPI_ARGMAX GEMM's keys (B * L rows, `slots` used, row
+ * stride ld): vasr_argmax_keys then vasr_ctc_collapse[_var] in ONE launch, one workgroup per
+ * utterance (the predictions stay in LDS; the fused CTC head + decode.py:46-69 of the
+ * reference's greedy path).  frames: NULL or device int32[B] as in vasr_ctc_collapse_var;
+ * pred: NULL or device int32[B * L] to also receive the per-frame argmax.  L <= 8192. */
+int vasr_ctc_collapse_keys(const uint64_t* keys, int64_t ld, int slots, int B, int L, const int32_t* frames,
+                           int blank, int collapse, int32_t* pred, int32_t* out_tokens, int32_t* out_len,
+                           int32_t* out_start, int32_t* out_end, void* stream);
 
 #ifdef __cplusplus
 }

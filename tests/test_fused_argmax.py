@@ -130,3 +130,74 @@ def test_graphed_transcriber_refuses_changed_weights(va):
     from velocity_asr.distributed import graphed_step
     with pytest.raises(RuntimeError, match="changed after capture"):
         graphed_step(gt)(gt.audio)
+
+
+@pytest.mark.parametrize("N", [5, 1000])
+@pytest.mark.parametrize("B,Lq", [(1, 1), (1, 63), (1, 64), (1, 65), (1, 501), (3, 130)])
+@pytest.mark.parametrize("collapse,timestamps,ragged", [(True, False, False), (False, False, False),
+                                                       (True, True, False), (True, False, True),
+                                                       (True, True, True)])
+def test_ctc_greedy_one_launch_matches_argmax_then_collapse(va, N, B, Lq, collapse, timestamps, ragged):
+    """vasr_ctc_collapse_keys (argmax keys + collapse in one launch) equals vasr_argmax_keys then
+    vasr_ctc_collapse[_var] exactly: tokens, lengths, timestamps, per-frame argmax; a 5-token
+    vocabulary gives long runs, repeats across blanks and empty outputs."""
+    from velocity_asr import _lib, ops
+    g = torch.Generator().manual_seed(B * 1000 + Lq + N)
+    K = 32
+    a = torch.randn(B * Lq, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.5).to(DEV)
+    bias[0] += 0.7  # blank frequent
+    frames = None
+    if ragged:
+        frames = torch.tensor([max(0, Lq - 17 * i) for i in range(B)], dtype=torch.int32).to(DEV)
+    pred = ops.gemm_argmax(a, w, bias).view(B, Lq)
+    want = ops.ctc_collapse(pred, 0, collapse, timestamps, frames=frames)
+    got = ops.gemm_ctc_greedy(a, w, bias, B, 0, collapse=collapse, timestamps=timestamps, frames=frames)
+    lens = want[1].cpu()
+    assert torch.equal(got[1].cpu(), lens)
+    for i in range(B):
+        n = int(lens[i])
+        assert torch.equal(got[0][i, :n].cpu(), want[0][i, :n].cpu())
+        if timestamps:
+            assert torch.equal(got[2][i, :n].cpu(), want[2][i, :n].cpu())
+            assert torch.equal(got[3][i, :n].cpu(), want[3][i, :n].cpu())
+    # the per-frame argmax output of the same launch
+    keys, slots, M = ops._gemm_argmax_keys(a, w, bias, None, None, "t")
+    p2 = torch.empty(M, dtype=torch.int32, device=DEV)
+    t2 = torch.empty((B, Lq), dtype=torch.int32, device=DEV)
+    l2 = torch.empty(B, dtype=torch.int32, device=DEV)
+    L = _lib.lib()
+    assert L.vasr_ctc_collapse_keys(keys.data_ptr(), slots, slots, B, Lq, None, 0, 1, p2.data_ptr(), t2.data_ptr(),
+                                    l2.data_ptr(), None, None, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(p2.view(B, Lq).cpu(), pred.cpu())
+
+
+def test_ctc_greedy_one_launch_argument_checks(va):
+    from velocity_asr import _lib
+    L = _lib.lib()
+    x = torch.zeros(16, dtype=torch.int64, device=DEV)
+    o = torch.zeros(16, dtype=torch.int32, device=DEV)
+    assert L.vasr_ctc_collapse_keys(x.data_ptr(), 1, 1, 1, 9000, None, 0, 1, None, o.data_ptr(), o.data_ptr(), None,
+                                    None, None) == -1
+    assert b"L <= 8192" in L.vasr_last_error()
+    assert L.vasr_ctc_collapse_keys(x.data_ptr(), 1, 2, 1, 4, None, 0, 1, None, o.data_ptr(), o.data_ptr(), None,
+                                    None, None) == -1
+
+
+def test_model_greedy_token_ids_match_reference(va):
+    """The pipeline's default decode (greedy_token_ids: head GEMM, then argmax + collapse in one
+    launch) gives the reference goldens' collapsed tokens."""
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    from velocity_asr import ops
+    for fname, (B, S_, seed) in (("fwd_b2_10s.npz", (2, 160000, 1234)), ("fwd_b2_3s.npz", (2, 48000, 21))):
+        mel = va.compute_mel_spectrogram(torch.from_numpy(S.make_audio(B, S_, seed=seed)).to(DEV))
+        toks, lens = m.greedy_token_ids(mel)
+        t2, l2, _, _ = ops.ctc_collapse(torch.from_numpy(golden(fname)["tokens"].astype(np.int32)).to(DEV))
+        assert torch.equal(lens.cpu(), l2.cpu())
+        for i in range(B):
+            assert torch.equal(toks[i, : int(lens[i])].cpu(), t2[i, : int(l2[i])].cpu())

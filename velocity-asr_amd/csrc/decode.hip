@@ -45,15 +45,12 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ x
 // prev-token loop, since prev is None after a blank and equals pred[t-1] otherwise.  Kept
 // frames are compacted with a ballot + popcount prefix.  A kept token's end frame is the
 // next run start (the first frame whose value differs), matching decode.py:89-123.
-// frames (optional): utterance b collapses its own first frames[b] rows (row stride stays L).
-__global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict__ pred, int ldL, int blank, int collapse,
-                                                      int32_t* __restrict__ toks, int32_t* __restrict__ lens,
-                                                      int32_t* __restrict__ st, int32_t* __restrict__ en,
-                                                      const int32_t* __restrict__ frames) {
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int L = frames ? frames[b] : ldL;
-    const int32_t* p = pred + (int64_t)b * ldL;
+// p: the utterance's frame predictions (global memory or LDS); its first L frames collapse
+// (outputs at row stride ldL).
+__device__ __forceinline__ void collapse_wave(const int32_t* p, int L, int ldL, int b, int blank, int collapse,
+                                              int32_t* __restrict__ toks, int32_t* __restrict__ lens,
+                                              int32_t* __restrict__ st, int32_t* __restrict__ en) {
+    const int lane = threadIdx.x & 63;
     int32_t* o = toks + (int64_t)b * ldL;
     int base = 0;  // tokens kept before this window
     for (int t0 = 0; t0 < L; t0 += 64) {
@@ -80,6 +77,43 @@ __global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict_
         lens[b] = base;
         if (st && L > 0 && p[L - 1] != blank && base > 0) en[(int64_t)b * ldL + base - 1] = L;
     }
+}
+
+// frames (optional): utterance b collapses its own first frames[b] rows (row stride stays L).
+__global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict__ pred, int ldL, int blank, int collapse,
+                                                      int32_t* __restrict__ toks, int32_t* __restrict__ lens,
+                                                      int32_t* __restrict__ st, int32_t* __restrict__ en,
+                                                      const int32_t* __restrict__ frames) {
+    const int b = blockIdx.x;
+    collapse_wave(pred + (int64_t)b * ldL, frames ? frames[b] : ldL, ldL, b, blank, collapse, toks, lens, st, en);
+}
+
+// Argmax keys -> tokens -> collapse in one launch, one workgroup per utterance: its 256 threads
+// reduce a row each (the row's slot keys, as argmax_keys_kernel) into an LDS copy of the
+// utterance's predictions, then wave 0 collapses them (collapse_wave).  Saves the collapse's
+// launch and its read-back of the predictions (one utterance: ~4.5 us of ~0.58 ms).
+constexpr int kCollapseKeysMaxL = 8192;
+__global__ __launch_bounds__(256) void collapse_keys_kernel(const unsigned long long* __restrict__ keys, int64_t ld,
+                                                            int slots, int ldL, const int32_t* __restrict__ frames,
+                                                            int blank, int collapse, int32_t* __restrict__ pred,
+                                                            int32_t* __restrict__ toks, int32_t* __restrict__ lens,
+                                                            int32_t* __restrict__ st, int32_t* __restrict__ en) {
+    __shared__ int32_t sp[kCollapseKeysMaxL];
+    const int b = blockIdx.x;
+    for (int t = threadIdx.x; t < ldL; t += 256) {
+        const unsigned long long* kr = keys + ((int64_t)b * ldL + t) * ld;
+        unsigned long long k = 0ull;
+#pragma unroll 8
+        for (int s = 0; s < slots; ++s) {
+            const unsigned long long v = kr[s];
+            k = v > k ? v : k;
+        }
+        const int32_t tok = (int32_t)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull));
+        sp[t] = tok;
+        if (pred) pred[(int64_t)b * ldL + t] = tok;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) collapse_wave(sp, frames ? frames[b] : ldL, ldL, b, blank, collapse, toks, lens, st, en);
 }
 
 // One wave per two rows: lane l reads slot l % 32 of row 2w + l / 32 (coalesced), then a
@@ -142,6 +176,22 @@ VASR_API int vasr_ctc_collapse_var(const int32_t* pred, int B, int L, const int3
     VASR_CHECK_ARG(frames, "vasr_ctc_collapse_var: null frames");
     return ctc_collapse(pred, B, L, frames, blank, collapse, out_tokens, out_len, out_start, out_end, stream,
                         "vasr_ctc_collapse_var");
+}
+
+VASR_API int vasr_ctc_collapse_keys(const uint64_t* keys, int64_t ld, int slots, int B, int L, const int32_t* frames,
+                                    int blank, int collapse, int32_t* pred, int32_t* out_tokens, int32_t* out_len,
+                                    int32_t* out_start, int32_t* out_end, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(keys && out_tokens && out_len && slots >= 1 && ld >= slots, "vasr_ctc_collapse_keys: bad arguments");
+    VASR_CHECK_ARG((out_start == nullptr) == (out_end == nullptr), "vasr_ctc_collapse_keys: start/end must both be set");
+    VASR_CHECK_ARG(out_start == nullptr || collapse, "vasr_ctc_collapse_keys: timestamps need collapse=1");
+    VASR_CHECK_ARG(B >= 0 && L >= 0 && L <= kCollapseKeysMaxL, "vasr_ctc_collapse_keys: bad shape B=%d L=%d (L <= %d)", B,
+                   L, kCollapseKeysMaxL);
+    if (B == 0) return VASR_OK;
+    hipLaunchKernelGGL(collapse_keys_kernel, dim3(B), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const unsigned long long*>(keys), ld, slots, L, frames, blank, collapse, pred,
+                       out_tokens, out_len, out_start, out_end);
+    return launch_status("vasr_ctc_collapse_keys");
 }
 
 VASR_API int vasr_argmax_keys(const uint64_t* keys, int64_t ld, int slots, int rows, int32_t* out, void* stream) {

@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -96,6 +96,8 @@ _SIGNATURES = {
                             c_p], ctypes.c_int),
     "vasr_minmax_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p], ctypes.c_int),
     "vasr_argmax_keys": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),
+    "vasr_ctc_collapse_keys": ([c_p, c_i64] + [ctypes.c_int] * 3 + [c_p, ctypes.c_int, ctypes.c_int] + [c_p] * 6,
+                               ctypes.c_int),
     "vasr_ctc_beam_search": ([c_p, c_i64, c_i64] + [ctypes.c_int] * 5 + [c_p] * 5 + [c_p], ctypes.c_int),
     "vasr_ctc_beam_workspace_elems": ([ctypes.c_int, ctypes.c_int], c_i64),
     "vasr_ctc_collapse": ([c_p] + [ctypes.c_int] * 4 + [c_p, c_p, c_p, c_p, c_p], ctypes.c_int),

@@ -138,6 +138,17 @@ class CTCOutputHead(nn.Module):
         w, b, qp = Q.linear_parts(self.proj[2])
         return ops.gemm_argmax(x.reshape(B * L, D), w, b, qparams=qp, ln=(ln.weight, ln.bias, ln.eps)).view(B, L)
 
+    def greedy(self, x: torch.Tensor, blank: int = 0, out=None, rows=None):
+        """Greedy CTC decode of forward(x) -- argmax(x) then the collapse of decode.py:46-69 --
+        with the argmax and the collapse in one launch after the head GEMM: (tokens (B, L),
+        lengths (B,)) int32.  rows: per-utterance row counts (int32 (B,)) of a padded batch."""
+        B, L, D = x.shape
+        ln = self.proj[0]
+        w, b, qp = Q.linear_parts(self.proj[2])
+        toks, lens, _, _ = ops.gemm_ctc_greedy(x.reshape(B * L, D), w, b, B, blank, qparams=qp,
+                                               ln=(ln.weight, ln.bias, ln.eps), out=out, frames=rows)
+        return toks, lens
+
 
 class VELOCITYASR(nn.Module):
     """VELOCITY-ASR v2 (reference model.py:242-471)."""
@@ -224,6 +235,20 @@ class VELOCITYASR(nn.Module):
             x = self.local_ssm(x)
             x = self.global_context(x, lengths=lengths)
             return self.ctc_head.argmax(x)
+
+    def greedy_token_ids(self, mel_spectrogram: torch.Tensor, frames=None, blank: int = 0, out=None, rows=None):
+        """Collapsed greedy CTC tokens of forward(mel) on the device, (tokens (B, L), lengths (B,))
+        int32: token_ids + ops.ctc_collapse with the argmax and the collapse in one launch.
+        rows: per-utterance token-row counts (int32 (B,) on the device) of a padded batch."""
+        if mel_spectrogram.device.type != "cuda":
+            _lib.require_device()
+            raise RuntimeError("velocity_asr (MI355X build): greedy_token_ids needs HIP tensors")
+        lengths = self._token_lengths(frames, mel_spectrogram.shape[1])
+        with torch.no_grad():
+            x = self.temporal_binding(mel_spectrogram.to(torch.float32))
+            x = self.local_ssm(x)
+            x = self.global_context(x, lengths=lengths)
+            return self.ctc_head.greedy(x, blank, out=out, rows=rows)
 
     def get_output_length(self, input_length: int) -> int:
         return (input_length + 1) // 2

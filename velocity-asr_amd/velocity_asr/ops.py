@@ -293,23 +293,19 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
     return out
 
 
-def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
-                qparams: Optional[torch.Tensor] = None, ln=None) -> torch.Tensor:
-    """int32 argmax over the N outputs of a @ w.T + bias (after qparams) per row, fused into the
-    GEMM epilogue (VASR_EPI_ARGMAX): the (M, N) product is never written.  Ties -> first index.
-    ln = (weight, bias, eps): LayerNorm each row of `a` first."""
-    _cuda_f32("gemm_argmax.a", a)
+def _gemm_argmax_keys(a: torch.Tensor, w: torch.Tensor, bias, qparams, ln, who: str):
+    """The VASR_EPI_ARGMAX GEMM: (M, ceil(N/32)) uint64 partial keys of a @ w.T + bias per row."""
+    _cuda_f32(f"{who}.a", a)
     args = GemmArgs()
     a = _ln_prologue(a, ln)
-    _cuda_w("gemm_argmax.w", w)
+    _cuda_w(f"{who}.w", w)
     bias = f32(bias)
-    M, K, lda = _rows("gemm_argmax.a", a)
-    N, Kw, ldw = _rows("gemm_argmax.w", w)
+    M, K, lda = _rows(f"{who}.a", a)
+    N, Kw, ldw = _rows(f"{who}.w", w)
     if Kw != K:
-        raise ValueError(f"gemm_argmax: a has K={K} but w has K={Kw}")
+        raise ValueError(f"{who}: a has K={K} but w has K={Kw}")
     slots = (N + 31) // 32
     keys = torch.empty((M, slots), device=a.device, dtype=torch.int64)  # every slot is written
-    out = torch.empty(M, device=a.device, dtype=torch.int32)
     args.A, args.lda, args.stride_a = a.data_ptr(), lda, 0
     args.W, args.ldw = w.data_ptr(), ldw
     args.bias = ptr(bias)
@@ -320,8 +316,35 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     ev = _t0("gemm")
     _linear(args, w, stream_of(a))
     _t1("gemm", ev, dict(M=M, N=N, K=K, batch=1))
-    check(L.lib().vasr_argmax_keys(keys.data_ptr(), slots, slots, M, out.data_ptr(), stream_of(a)), "vasr_argmax_keys")
+    return keys, slots, M
+
+
+def gemm_argmax(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+                qparams: Optional[torch.Tensor] = None, ln=None) -> torch.Tensor:
+    """int32 argmax over the N outputs of a @ w.T + bias (after qparams) per row, fused into the
+    GEMM epilogue (VASR_EPI_ARGMAX): the (M, N) product is never written.  Ties -> first index.
+    ln = (weight, bias, eps): LayerNorm each row of `a` first."""
+    keys, slots, M = _gemm_argmax_keys(a, w, bias, qparams, ln, "gemm_argmax")
+    out = torch.empty(M, device=a.device, dtype=torch.int32)
+    check(L.lib().vasr_argmax_keys(keys.data_ptr(), slots, slots, M, out.data_ptr(), stream_of(keys)), "vasr_argmax_keys")
     return out
+
+
+def gemm_ctc_greedy(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], B: int, blank: int = 0, *,
+                    qparams: Optional[torch.Tensor] = None, ln=None, collapse: bool = True, timestamps: bool = False,
+                    out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, frames: Optional[torch.Tensor] = None):
+    """Greedy CTC decode of B utterances (a: B * L rows) straight from the argmax GEMM's keys:
+    argmax + collapse in one launch (vasr_ctc_collapse_keys); same results as gemm_argmax then
+    ctc_collapse.  Returns (tokens, lengths, start, end) as ctc_collapse."""
+    keys, slots, M = _gemm_argmax_keys(a, w, bias, qparams, ln, "gemm_ctc_greedy")
+    if B <= 0 or M % B:
+        raise ValueError(f"gemm_ctc_greedy: {M} rows do not split into B={B} utterances")
+    Lq = M // B
+    toks, lens, st, en, frames = _collapse_outputs("gemm_ctc_greedy", B, Lq, keys.device, out, timestamps, frames)
+    check(L.lib().vasr_ctc_collapse_keys(keys.data_ptr(), slots, slots, B, Lq, ptr(frames), int(blank), int(collapse),
+                                         None, toks.data_ptr(), lens.data_ptr(), ptr(st), ptr(en), stream_of(keys)),
+          "vasr_ctc_collapse_keys")
+    return toks, lens, st, en
 
 
 def gemm_batched(a_base: torch.Tensor, lda: int, stride_a: int, rows: int, batch: int, K: int, w: torch.Tensor,
@@ -667,6 +690,24 @@ def argmax(logits: torch.Tensor) -> torch.Tensor:
     return out.view(logits.shape[:-1])
 
 
+def _collapse_outputs(who: str, B: int, Lq: int, device, out, timestamps: bool, frames):
+    """Output buffers (tokens, lengths, start, end) of a collapse and its checked frames."""
+    if out is None:
+        toks = torch.empty((B, Lq), device=device, dtype=torch.int32)
+        lens = torch.empty((B,), device=device, dtype=torch.int32)
+    else:
+        toks, lens = out
+        for n, t, shape in (("tokens", toks, (B, Lq)), ("lengths", lens, (B,))):
+            if (t.device != device or t.dtype != torch.int32 or tuple(t.shape) != shape
+                    or not t.is_contiguous()):
+                raise ValueError(f"{who}: out {n} must be a contiguous int32 {shape} tensor on {device}")
+    st = en = None
+    if timestamps:
+        st = torch.empty((B, Lq), device=device, dtype=torch.int32)
+        en = torch.empty((B, Lq), device=device, dtype=torch.int32)
+    return toks, lens, st, en, _lens(f"{who}.frames", frames, B, device)
+
+
 def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, timestamps: bool = False,
                  out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, frames: Optional[torch.Tensor] = None):
     """Device-side greedy CTC collapse of (B, L) int32 predictions.  out = (tokens (B, L),
@@ -676,20 +717,7 @@ def ctc_collapse(pred: torch.Tensor, blank: int = 0, collapse: bool = True, time
         raise TypeError("ctc_collapse: expected a cuda int32 tensor")
     pred = pred.contiguous()
     B, Lq = pred.shape
-    if out is None:
-        toks = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
-        lens = torch.empty((B,), device=pred.device, dtype=torch.int32)
-    else:
-        toks, lens = out
-        for n, t, shape in (("tokens", toks, (B, Lq)), ("lengths", lens, (B,))):
-            if (t.device != pred.device or t.dtype != torch.int32 or tuple(t.shape) != shape
-                    or not t.is_contiguous()):
-                raise ValueError(f"ctc_collapse: out {n} must be a contiguous int32 {shape} tensor on {pred.device}")
-    st = en = None
-    if timestamps:
-        st = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
-        en = torch.empty((B, Lq), device=pred.device, dtype=torch.int32)
-    frames = _lens("ctc_collapse.frames", frames, B, pred.device)
+    toks, lens, st, en, frames = _collapse_outputs("ctc_collapse", B, Lq, pred.device, out, timestamps, frames)
     if frames is None:
         check(L.lib().vasr_ctc_collapse(pred.data_ptr(), B, Lq, int(blank), int(collapse), toks.data_ptr(),
                                         lens.data_ptr(), ptr(st), ptr(en), stream_of(pred)), "vasr_ctc_collapse")

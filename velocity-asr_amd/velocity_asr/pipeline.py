@@ -1,8 +1,8 @@
 """Batch transcription pipeline on the device: audio (B, S) -> tokens, no host round trip.
 
     mel (real-FFT |STFT|^2 straight from the unpadded audio + log-mel; other n_fft / hop: reflect
-    pad + DFT GEMM)  ->  VELOCITYASR.token_ids (forward with the CTC head's row argmax fused into
-    its GEMM)  ->  CTC collapse
+    pad + DFT GEMM)  ->  VELOCITYASR.greedy_token_ids (forward with the CTC head's row argmax
+    fused into its GEMM, then the argmax keys and the CTC collapse in one launch)
 
 Everything stays in HBM; the only device->host traffic is the (B, L) int32 token block
 and lengths when the caller asks for Python lists.  ``GraphedTranscriber`` captures the
@@ -26,6 +26,8 @@ from .model import VELOCITYASR
 
 # VASR_FUSED_ARGMAX=0 selects logits + a separate argmax pass (diagnostic comparison)
 FUSED_ARGMAX = os.environ.get("VASR_FUSED_ARGMAX", "1") != "0"
+# VASR_COLLAPSE_KEYS=0: the argmax keys and the collapse as two launches (A/B comparison)
+COLLAPSE_KEYS = os.environ.get("VASR_COLLAPSE_KEYS", "1") != "0"
 
 
 def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0,
@@ -40,13 +42,14 @@ def audio_to_token_ids(model: VELOCITYASR, audio: torch.Tensor, blank: int = 0,
     mel = mel_on_device(audio, SAMPLE_RATE, N_FFT, HOP_LENGTH, model.config.mel_bins, lengths=lengths,
                         frame_pad=model.temporal_binding.conv_padding())
     frames = None if lengths is None else [int(v) // HOP_LENGTH + 1 for v in lengths]
-    if FUSED_ARGMAX:
-        pred = model.token_ids(mel, frames=frames)  # CTC head GEMM with the row argmax fused: no logits in HBM
-    else:
-        pred = ops.argmax(model(mel, frames=frames))
     rows = None
     if frames is not None:
         rows = torch.tensor([model.get_output_length(f) for f in frames], dtype=torch.int32).to(audio.device)
+    if FUSED_ARGMAX and COLLAPSE_KEYS:
+        # CTC head GEMM with the row argmax fused (no logits in HBM), then argmax keys + collapse
+        # in one launch
+        return model.greedy_token_ids(mel, frames=frames, blank=blank, out=out, rows=rows)
+    pred = model.token_ids(mel, frames=frames) if FUSED_ARGMAX else ops.argmax(model(mel, frames=frames))
     toks, lens, _, _ = ops.ctc_collapse(pred, blank, True, False, out=out, frames=rows)
     return toks, lens
 
