@@ -52,8 +52,9 @@ enum vasr_option {
     VASR_OPT_GEMM_ENGINE = 3, /* split-bf16 GEMM main loop: 0 auto, 1 LDS-ring tiles, 2 A-rows-stationary
                                  (K = 128 / 192, batch 1, unpaired epilogues) (VASR_GEMM_ENGINE)         */
     VASR_OPT_TAIL_WAVES = 4,  /* waves per fused-SSMBlock-tail workgroup: 0, 4, 6, 12 (VASR_TAIL_WAVES)    */
-    VASR_OPT_SCAN_SPLIT = 5   /* form of vasr_ssm_scan_chunked_f32: 0 auto, 1 three launches, 2 one launch
+    VASR_OPT_SCAN_SPLIT = 5,  /* form of vasr_ssm_scan_chunked_f32: 0 auto, 1 three launches, 2 one launch
                                  (time split inside the workgroup) (VASR_SCAN_SPLIT)                     */
+    VASR_OPT_DW_ROWS = 6      /* output rows per vasr_ln_dwconv_f32 workgroup: 0 auto, 4, 8, 16 (VASR_DW_ROWS) */
 };
 int vasr_set_option(int key, int value);
 

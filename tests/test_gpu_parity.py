@@ -164,6 +164,26 @@ def test_layer_norm_and_dwconv(va, L, C, Kc):
     np.testing.assert_allclose(y, R.causal_dwconv(R.layer_norm(x, w, b), cw, cb), atol=3e-5, rtol=1e-5)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,C,Kc", [(1, 501, 192, 4), (3, 64, 192, 4), (2, 37, 192, 4), (2, 3, 192, 4),
+                                      (1, 40, 96, 2), (2, 33, 256, 7)])
+def test_ln_dwconv_tile_heights_bitwise(va, B, L, C, Kc):
+    """vasr_ln_dwconv_f32's workgroup tile heights (VASR_OPT_DW_ROWS 4 / 8 / 16; auto picks 8
+    below 512 workgroups of 16) give bitwise the same outputs."""
+    import torch
+    from velocity_asr import _lib, ops
+    rng = np.random.default_rng(B * 1000 + L + Kc)
+    x = t(rng.standard_normal((B, L, C)).astype(np.float32) * 2 + 0.5)
+    w, b = t((1 + 0.1 * rng.standard_normal(C)).astype(np.float32)), t((0.1 * rng.standard_normal(C)).astype(np.float32))
+    cw, cb = t((0.3 * rng.standard_normal((C, Kc))).astype(np.float32)), t((0.1 * rng.standard_normal(C)).astype(np.float32))
+    ys = []
+    for rows in (0, 4, 8, 16):
+        with ops.option(_lib.OPT_DW_ROWS, rows):
+            ys.append(ops.ln_dwconv(x, w, b, cw, cb))
+    for y in ys[1:]:
+        assert torch.equal(y, ys[0])
+
+
 def _scan_cases():
     meta = json.loads(str(golden("scan.npz")["meta"]))
     return [tuple(c) for c in meta["cases"]]

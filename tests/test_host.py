@@ -63,7 +63,7 @@ def test_tuning_options():
     L = _lib.load()
     for key, allowed in ((_lib.OPT_SCAN_LANES, (2, 4)), (_lib.OPT_SCAN_CHUNK, (16, 32)), (_lib.OPT_TAIL_ROWS, (16, 32)),
                          (_lib.OPT_GEMM_ENGINE, (1, 2)), (_lib.OPT_TAIL_WAVES, (4, 6, 12)),
-                         (_lib.OPT_SCAN_SPLIT, (1, 2))):
+                         (_lib.OPT_SCAN_SPLIT, (1, 2)), (_lib.OPT_DW_ROWS, (4, 8, 16))):
         base = L.vasr_set_option(key, -1)
         assert base in (0,) + allowed
         for v in allowed:

@@ -32,18 +32,25 @@ def timed(fn, iters=20, reps=5):
     return a.elapsed_time(b) * 1e3 / (iters * reps)
 
 
+def digest(t):
+    """Order-independent bit digest of a float tensor (variants compared bitwise)."""
+    return int(t.contiguous().view(torch.int32).to(torch.int64).sum().item()) & 0xFFFFFFFF
+
+
 def main():
     _lib.require_device()
     C, L = 192, 501
-    w, bb = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
-    cw, cb = torch.randn(C, 4, device="cuda"), torch.randn(C, device="cuda")
-    for B in (16, 32):
-        x = torch.randn(B, L, C, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    w, bb = torch.randn(C, device="cuda", generator=g), torch.randn(C, device="cuda", generator=g)
+    cw, cb = torch.randn(C, 4, device="cuda", generator=g), torch.randn(C, device="cuda", generator=g)
+    for B in (1, 16, 32):
+        x = torch.randn(B, L, C, device="cuda", generator=g)
         byt = 2 * x.numel() * 4
         t_ln = timed(lambda: ops.layer_norm(x, w, bb))
         t_dw = timed(lambda: ops.ln_dwconv(x, w, bb, cw, cb))
-        print(f"B={B}: layer_norm {t_ln:.1f} us ({byt / t_ln / 1e3:.0f} GB/s), ln_dwconv {t_dw:.1f} us "
-              f"({byt / t_dw / 1e3:.0f} GB/s)", flush=True)
+        d_ln, d_dw = digest(ops.layer_norm(x, w, bb)), digest(ops.ln_dwconv(x, w, bb, cw, cb))
+        print(f"B={B}: layer_norm {t_ln:.2f} us ({byt / t_ln / 1e3:.0f} GB/s), ln_dwconv {t_dw:.2f} us "
+              f"({byt / t_dw / 1e3:.0f} GB/s) digests {d_ln:08x} {d_dw:08x}", flush=True)
 
 
 if __name__ == "__main__":

@@ -28,11 +28,11 @@ VASR_API const char* vasr_last_error(void) { return vasr::g_last_error; }
 
 // Tuning options (vasr_set_option): process-wide, defaults from the environment read once.
 namespace {
-constexpr int kNumOptions = 6;
+constexpr int kNumOptions = 7;
 const char* const kOptionEnv[kNumOptions] = {"VASR_SCAN_NPL", "VASR_SCAN_T", "VASR_TAIL_ROWS", "VASR_GEMM_ENGINE",
-                                               "VASR_TAIL_WAVES", "VASR_SCAN_SPLIT"};
+                                               "VASR_TAIL_WAVES", "VASR_SCAN_SPLIT", "VASR_DW_ROWS"};
 const int kOptionValues[kNumOptions][4] = {{0, 2, 4, -1}, {0, 16, 32, -1}, {0, 16, 32, -1},
-                                           {0, 1, 2, -1}, {0, 4, 6, 12},   {0, 1, 2, -1}};
+                                           {0, 1, 2, -1}, {0, 4, 6, 12},   {0, 1, 2, -1}, {0, 4, 8, 16}};
 std::atomic<int> g_options[kNumOptions];
 std::once_flag g_options_once;
 

@@ -56,10 +56,12 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
     ln_row_to<CPL>(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
 }
 
-#ifndef VASR_DW_TT
-#define VASR_DW_TT 16
-#endif
-constexpr int TT = VASR_DW_TT;  // output rows per block (1024 blocks at B=32, L=501: 4 per CU)
+// TT: output rows per block -- 16 for full-chip launches (1024 blocks at B = 32, L = 501: 4 per
+// CU), 8 below 1024 blocks of 16, 4 below 128 (graph-timed at L = 501, bitwise the same outputs:
+// B = 1 2.74 / 3.18 / 4.09 us at 4 / 8 / 16 rows, B = 16 5.69 / 5.28 / 5.65, B = 32 9.11 / 8.39 /
+// 8.31; 32 rows slower everywhere.  Measured and dropped (patch in profiles/r05at/): a wave-tiled
+// form with the causal window in registers (no LDS, no barrier: 8.13 vs 8.35 us at B = 32, slower
+// below) and LayerNorm with 2 / 4 rows per wave (5.8 / 6.2 vs 5.5 us at B = 32))
 constexpr int kMaxC = 256;   // LDS row capacity
 constexpr int kMaxK = 8;
 
@@ -74,7 +76,7 @@ constexpr int kMaxK = 8;
 // 0 = generic (C <= kMaxC, guarded columns).  The channel's taps and bias are loaded before
 // phase 1 (C <= kMaxC = 256 threads: one channel per thread), so their latency overlaps the
 // row loads instead of following the barrier.
-template <int KC, int CPT>
+template <int KC, int CPT, int TT>
 __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b,
@@ -239,13 +241,23 @@ VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* 
     VASR_CHECK_ARG(C > 0 && C <= kMaxC && Kc >= 1 && Kc <= kMaxK && B >= 0 && L >= 0,
                    "vasr_ln_dwconv_f32: unsupported shape C=%d Kc=%d", C, Kc);
     if (B == 0 || L == 0) return VASR_OK;
-    const dim3 grid((L + TT - 1) / TT, B), block(256);
+    const dim3 block(256);
     hipStream_t s = as_stream(stream);
-    if (Kc == 4 && C == 192)
-        hipLaunchKernelGGL((ln_dwconv_kernel<4, 3>), grid, block, 0, s, x, ln_w, ln_b, conv_w, conv_b, y, L, C, Kc, eps);
-    else if (Kc == 4)
-        hipLaunchKernelGGL((ln_dwconv_kernel<4, 0>), grid, block, 0, s, x, ln_w, ln_b, conv_w, conv_b, y, L, C, Kc, eps);
-    else
-        hipLaunchKernelGGL((ln_dwconv_kernel<0, 0>), grid, block, 0, s, x, ln_w, ln_b, conv_w, conv_b, y, L, C, Kc, eps);
+    const int n16 = B * ((L + 15) / 16);  // workgroups at 16 rows
+    const int tt = option(VASR_OPT_DW_ROWS) ? option(VASR_OPT_DW_ROWS) : n16 < 128 ? 4 : n16 < 1024 ? 8 : 16;
+#define VASR_DW(KC, CPT, TT)                                                                                     \
+    hipLaunchKernelGGL((ln_dwconv_kernel<KC, CPT, TT>), dim3((L + TT - 1) / TT, B), block, 0, s, x, ln_w, ln_b, \
+                       conv_w, conv_b, y, L, C, Kc, eps)
+#define VASR_DW_TT(KC, CPT) \
+    if (tt == 4) VASR_DW(KC, CPT, 4); else if (tt == 8) VASR_DW(KC, CPT, 8); else VASR_DW(KC, CPT, 16)
+    if (Kc == 4 && C == 192) {
+        VASR_DW_TT(4, 3);
+    } else if (Kc == 4) {
+        VASR_DW_TT(4, 0);
+    } else {
+        VASR_DW_TT(0, 0);
+    }
+#undef VASR_DW_TT
+#undef VASR_DW
     return launch_status("vasr_ln_dwconv_f32");
 }

@@ -23,7 +23,7 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "include", "vasr.
 
 (EPI_NONE, EPI_GELU, EPI_SOFTPLUS_FROM, EPI_RESIDUAL, EPI_GELU_PE, EPI_PAIR_POWER, EPI_PAIR_FUSION,
  EPI_ARGMAX) = range(8)
-OPT_SCAN_LANES, OPT_SCAN_CHUNK, OPT_TAIL_ROWS, OPT_GEMM_ENGINE, OPT_TAIL_WAVES, OPT_SCAN_SPLIT = range(6)  # enum vasr_option
+OPT_SCAN_LANES, OPT_SCAN_CHUNK, OPT_TAIL_ROWS, OPT_GEMM_ENGINE, OPT_TAIL_WAVES, OPT_SCAN_SPLIT, OPT_DW_ROWS = range(7)  # enum vasr_option
 
 c_i32, c_i64, c_f32, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
