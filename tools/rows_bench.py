@@ -46,6 +46,19 @@ def main():
         flops = 6 * 2.0 * M * 1280 * 192
         print(f"lib={os.path.basename(lib)} M={M}: rows {t_rows:.2f} us ({flops / t_rows / 1e6:.0f} bf16-TF/s), "
               f"tiles {t_tiles:.2f} us, bitwise equal {same}", flush=True)
+        # the same projection without the 384 z columns (z formed elsewhere):
+        # [x | B | C | dt], softplus from column 512
+        w_noz = torch.cat([w[:384], w[768:]]).contiguous()
+        b_noz = torch.cat([b[:384], b[768:]]).contiguous()
+        out_noz = torch.empty(M, 896, device="cuda")
+
+        def run_noz():
+            return ops.gemm(u, w_noz, b_noz, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=512, out=out_noz)
+        t_noz = timed(run_noz)
+        noz = run_noz()
+        same_noz = torch.equal(noz.view(torch.int32), torch.cat([rows[:, :384], rows[:, 768:]], 1).view(torch.int32))
+        print(f"lib={os.path.basename(lib)} M={M}: without z (N = 896) rows {t_noz:.2f} us, "
+              f"columns bitwise equal to the 1280-column launch's {same_noz}", flush=True)
 
 
 if __name__ == "__main__":
