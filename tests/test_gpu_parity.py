@@ -184,6 +184,32 @@ def test_ln_dwconv_tile_heights_bitwise(va, B, L, C, Kc):
         assert torch.equal(y, ys[0])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("lengths", [None, (16000, 9000, 12345)])
+def test_mel_batch_invariant_bitwise(va, lengths):
+    """An utterance's log-mel (per-utterance statistics from fp64 chunk partials summed in a fixed
+    order) is bitwise the same alone, in a pair and in a batch of three, with and without
+    per-utterance lengths, and in the zero-framed layout the temporal conv reads."""
+    import torch
+    from velocity_asr import audio as A, ops
+    rng = np.random.default_rng(5)
+    audio = t((0.1 * rng.standard_normal((3, 16000))).astype(np.float32))
+    lens = None if lengths is None else torch.tensor(lengths, dtype=torch.int32)
+    full = A.compute_mel_spectrogram(audio, lengths=lens)
+    for i in range(3):
+        one = A.compute_mel_spectrogram(audio[i:i + 1].contiguous(), lengths=None if lens is None else lens[i:i + 1])
+        assert torch.equal(one[0], full[i])
+    two = A.compute_mel_spectrogram(audio[:2].contiguous(), lengths=None if lens is None else lens[:2])
+    assert torch.equal(two, full[:2])
+    if lens is None:  # the zero-framed layout the temporal conv reads (frame_pad = 1)
+        tb = A._tables(audio.device, 400, 80, 16000)
+        power = ops.stft_power_400(audio, tb.window)
+        F = power.shape[1]
+        z3 = ops.mel_log_norm(power, tb.n_bins, F * tb.n_bins, tb.fb_csr, 3, F, 80, True, frame_pad=1)
+        z1 = ops.mel_log_norm(power[:1].contiguous(), tb.n_bins, F * tb.n_bins, tb.fb_csr, 1, F, 80, True, frame_pad=1)
+        assert torch.equal(z1._vasr_zero_framed[0][0], z3._vasr_zero_framed[0][0])
+
+
 def _scan_cases():
     meta = json.loads(str(golden("scan.npz")["meta"]))
     return [tuple(c) for c in meta["cases"]]
