@@ -38,6 +38,12 @@ def main():
               f"WAIT_INST_ANY/WAVE_CYCLES {m.get('SQ_WAIT_INST_ANY', 0) / wc:.3f} "
               f"WAIT_ANY/WAVE_CYCLES {m.get('SQ_WAIT_ANY', 0) / wc:.3f} "
               f"ACTIVE_INST_VALU/WAVE_CYCLES {m.get('SQ_ACTIVE_INST_VALU', 0) / wc:.3f}")
+    if m.get("GRBM_GUI_ACTIVE") and m.get("SQ_ACTIVE_INST_VALU"):
+        # GRBM_GUI_ACTIVE sums the 8 XCDs' clocks; SQ_ACTIVE_INST_* count quad-cycles over all waves
+        cyc = m["GRBM_GUI_ACTIVE"] / 8
+        print(f"kernel cycles {cyc:.4g}; SIMD VALU busy (ACTIVE_INST_VALU x 4 / (1024 SIMDs x cycles)) "
+              f"{4 * m['SQ_ACTIVE_INST_VALU'] / (1024 * cyc):.3f}; SIMD issue busy (ACTIVE_INST_ANY x 4 / "
+              f"(1024 x cycles)) {4 * m.get('SQ_ACTIVE_INST_ANY', 0) / (1024 * cyc):.3f}")
 
 
 if __name__ == "__main__":
