@@ -210,6 +210,26 @@ def test_mel_batch_invariant_bitwise(va, lengths):
         assert torch.equal(z1._vasr_zero_framed[0][0], z3._vasr_zero_framed[0][0])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,K", [(501, 64), (64, 16), (501, 16), (37, 5), (9, 9), (300, 7)])
+def test_adaptive_pool_sums_rows_in_order(va, L, K):
+    """vasr_adaptive_pool_f32 adds each window's rows in row order (fp32, one rounding per add;
+    windows of 1 to 72 rows, loaded 8 at a time): bitwise equal to that sum done on the host."""
+    from velocity_asr import ops
+    rng = np.random.default_rng(L * 100 + K)
+    B, C = 2, 192
+    x = rng.standard_normal((B, L, C)).astype(np.float32)
+    got = ops.adaptive_pool(t(x), K).cpu().numpy()
+    want = np.empty((B, K, C), np.float32)
+    for i in range(K):
+        s, e = (i * L) // K, ((i + 1) * L + K - 1) // K
+        acc = np.zeros((B, C), np.float32)
+        for r in range(s, e):
+            acc = (acc + x[:, r]).astype(np.float32)
+        want[:, i] = acc / np.float32(e - s)
+    assert np.array_equal(got, want)
+
+
 def _scan_cases():
     meta = json.loads(str(golden("scan.npz")["meta"]))
     return [tuple(c) for c in meta["cases"]]

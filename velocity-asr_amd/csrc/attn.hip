@@ -29,8 +29,17 @@ __global__ void adaptive_pool_kernel(const float* __restrict__ x, float* __restr
     const int s = (int)(((int64_t)i * Lb) / Kb);
     const int e = (int)(((int64_t)(i + 1) * Lb + Kb - 1) / Kb);
     const float* xb = x + ((int64_t)b * L) * C + c;
+    // the window's rows loaded 8 at a time before they are added (independent loads in flight
+    // instead of one load latency per row), then added in row order: the same sum as a plain loop
     float acc = 0.f;
-    for (int t = s; t < e; ++t) acc += xb[(int64_t)t * C];
+    for (int t0 = s; t0 < e; t0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = t0 + j < e ? xb[(int64_t)(t0 + j) * C] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (t0 + j < e) acc += v[j];
+    }
     out[idx] = acc / (float)(e - s);
 }
 
