@@ -146,9 +146,26 @@ __global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restr
         const int fl = i / n_mels, m = i - fl * n_mels;
         const float* prow = rows + fl * ldp;
         float acc = 0.f;
-        if (csr_lds)
-            for (int e = rp_s[m]; e < rp_s[m + 1]; ++e) acc = __builtin_fmaf(val_s[e], prow[col_s[e]], acc);
-        else
+        if (csr_lds) {
+            // 8 entries' indices, weights and power values read before their fmas (independent
+            // LDS reads in flight instead of two dependent round trips per entry), fmas in
+            // entry order: the same sum
+            const int e1 = rp_s[m + 1];
+            for (int e0 = rp_s[m]; e0 < e1; e0 += 8) {
+                int cj[8];
+                float wj[8], pj[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    cj[j] = e0 + j < e1 ? col_s[e0 + j] : 0;
+                    wj[j] = e0 + j < e1 ? val_s[e0 + j] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pj[j] = prow[cj[j]];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (e0 + j < e1) acc = __builtin_fmaf(wj[j], pj[j], acc);
+            }
+        } else
             for (int e = rp_s[m]; e < rp_s[m + 1]; ++e) acc = __builtin_fmaf(val[e], prow[col[e]], acc);
         const float v = logf(acc + 1e-10f);
         vals[i] = v;
