@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 14
+#define VASR_ABI_VERSION 15
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -200,6 +200,10 @@ int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const float* dt, i
                               float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
                               float* workspace, int64_t workspace_floats, void* stream);
 int64_t vasr_ssm_scan_workspace_floats(int B, int L, int Di, int N);
+/* 1 when vasr_ssm_scan_chunked_f32 runs this shape as the one-launch time-split form under the
+ * current options (VASR_OPT_SCAN_SPLIT / VASR_OPT_SCAN_LANES), else 0: the launcher's own rule,
+ * for hosts that choose between the streaming and chunked entry points (ABI 15). */
+int vasr_ssm_scan_split_selected(int B, int L, int Di, int N);
 
 /* ------------------------------------------------------------------ SSMBlock tail, fused
  * The tail of SSMBlock._forward_impl (ssm.py:415-425) in one launch for d_model D = 192 and
@@ -368,7 +372,8 @@ int64_t vasr_ctc_beam_workspace_elems(int L, int W);
 int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int collapse,
                       int32_t* out_tokens, int32_t* out_len, int32_t* out_start,
                       int32_t* out_end, void* stream);
-/* frames[b] (device, 0 <= frames[b] <= L): utterance b collapses its own first frames[b] rows. */
+/* frames[b] (device): utterance b collapses its own first frames[b] rows; values outside [0, L]
+ * are clamped to it (no row past L is read or written). */
 int vasr_ctc_collapse_var(const int32_t* pred, int B, int L, const int32_t* frames, int blank, int collapse,
                           int32_t* out_tokens, int32_t* out_len, int32_t* out_start, int32_t* out_end,
                           void* stream);

@@ -138,7 +138,12 @@ def test_autotuned_schedule_matches_eager(model):
     assert sorted(tried) == [1, 2] and len(tr.graphs) in (1, 2)
     assert torch.equal(tr.audio, audio)  # timed on (and holding) the clips it serves
     assert len(tr.autotune_rounds) >= 1 and all(sorted(r) == [1, 2] for r in tr.autotune_rounds)
-    tr.release_candidates()
+    assert not getattr(tr, "_candidates", None)  # the losers are freed by default
+    tr2, _ = autotuned_transcriber(model, 8, 48000, reps=2, rounds=1, audio=audio, keep_candidates=True)
+    assert len(tr2._candidates) == 1  # bench.py's opt-in: kept until release_candidates()
+    tr2.release_candidates()
+    assert not getattr(tr2, "_candidates", None)
+    del tr2
     for _ in range(3):
         tr.step()
         assert token_lists(*tr.collect()) == exp

@@ -174,6 +174,45 @@ def test_ctc_greedy_one_launch_matches_argmax_then_collapse(va, N, B, Lq, collap
     assert torch.equal(p2.view(B, Lq).cpu(), pred.cpu())
 
 
+def test_collapse_clamps_frames_to_the_row(va):
+    """frames[b] outside [0, L] is clamped: past L both collapse kernels read and
+    write only the utterance's own L rows (as frames = L); negative counts give no tokens.
+    Canary rows after the batch's outputs must stay untouched."""
+    from velocity_asr import _lib, ops
+    B, Lq, N, K = 3, 70, 7, 32
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(B * Lq, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.3).to(DEV)
+    pred = ops.gemm_argmax(a, w, bias).view(B, Lq)
+    full = ops.ctc_collapse(pred, 0, True, True)
+    frames = torch.tensor([Lq + 1000, -5, Lq], dtype=torch.int32, device=DEV)
+    L = _lib.lib()
+    for one_launch in (False, True):
+        canary = -7
+        toks = torch.full((B + 1, Lq), canary, dtype=torch.int32, device=DEV)
+        st = torch.full((B + 1, Lq), canary, dtype=torch.int32, device=DEV)
+        en = torch.full((B + 1, Lq), canary, dtype=torch.int32, device=DEV)
+        lens = torch.full((B,), canary, dtype=torch.int32, device=DEV)
+        if one_launch:
+            keys, slots, M = ops._gemm_argmax_keys(a, w, bias, None, None, "t")
+            rc = L.vasr_ctc_collapse_keys(keys.data_ptr(), slots, slots, B, Lq, frames.data_ptr(), 0, 1, None,
+                                          toks.data_ptr(), lens.data_ptr(), st.data_ptr(), en.data_ptr(), None)
+        else:
+            rc = L.vasr_ctc_collapse_var(pred.data_ptr(), B, Lq, frames.data_ptr(), 0, 1, toks.data_ptr(),
+                                         lens.data_ptr(), st.data_ptr(), en.data_ptr(), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert int(lens[1]) == 0
+        for b in (0, 2):  # past L -> the whole row, as frames = L
+            n = int(full[1][b])
+            assert int(lens[b]) == n
+            assert torch.equal(toks[b, :n].cpu(), full[0][b, :n].cpu())
+            assert torch.equal(st[b, :n].cpu(), full[2][b, :n].cpu()) and torch.equal(en[b, :n].cpu(), full[3][b, :n].cpu())
+        for t in (toks, st, en):
+            assert bool((t[B] == canary).all()), "wrote past the batch's rows"
+
+
 def test_ctc_greedy_one_launch_argument_checks(va):
     from velocity_asr import _lib
     L = _lib.lib()

@@ -216,6 +216,24 @@ def test_tree_scan_kernel_mode_selection(monkeypatch):
     assert ssm._SCAN_MODE_ID == {"parallel": 0, "sequential": 1, "mamba": 1}
 
 
+def test_scan_form_follows_the_library_rule():
+    """ops._use_chunked takes the library's own one-launch rule (vasr_ssm_scan_split_selected,
+    ABI 15) instead of a Python copy of scan.hip's condition; options change it."""
+    from velocity_asr import _lib, ops
+    lib = _lib.load()
+    sel = lib.vasr_ssm_scan_split_selected
+    assert sel(1, 501, 384, 64) == 1 and sel(1, 64, 384, 32) == 1  # one utterance: one launch
+    assert sel(1, 513, 384, 64) == 0 and sel(2, 501, 384, 64) == 0 and sel(1, 501, 384, 128) == 0
+    assert ops._use_chunked(1, 64, 384, 32, 2)  # short L, but the one-launch form
+    assert not ops._use_chunked(32, 501, 384, 64, 2)
+    with ops.option(_lib.OPT_SCAN_SPLIT, 1):  # three launches forced: short L stays streaming
+        assert sel(1, 64, 384, 32) == 0 and not ops._use_chunked(1, 64, 384, 32, 2)
+    with ops.option(_lib.OPT_SCAN_SPLIT, 2):
+        assert sel(2, 1000, 384, 64) == 1
+    with ops.option(_lib.OPT_SCAN_LANES, 4):
+        assert sel(1, 501, 384, 64) == 0
+
+
 def _isa_scan():
     sys.path.insert(0, os.path.join(REPO, "tools", "isa"))
     import isa_scan
@@ -273,3 +291,47 @@ def test_isa_guard_detects_the_slp_stft_sequence(tmp_path):
         found[tag] = isa.pk_swapped(ins)
     assert len(found["slp"]) >= 10, found["slp"]
     assert found["noslp"] == []
+
+
+_TEARDOWN_SCRIPT = r"""
+import sys
+sys.path[:0] = [{pkg!r}]
+import torch
+from velocity_asr import ops
+seen = []
+sys.unraisablehook = lambda u: seen.append(repr(u.exc_value))
+t = torch.zeros(8, 8, device={dev!r}, dtype={dtype})
+if {real!r}:  # the split planes of a weight, as the model builds them
+    ops.split_weights(t); ops.split_weights16(t)
+    torch.cuda.synchronize()
+else:  # an fp32 copy of a bf16 parameter: the same cache registration, no kernel
+    ops.f32(t)
+# what interpreter teardown did in the driver's runs (profiles/r05j/step_course.txt): the module's
+# _-prefixed globals are None (_PyModule_ClearDict's first pass) while a cache entry and its
+# weakref are still alive, and then the weight dies
+alive = {{k: v for k, v in vars(ops).items() if k.startswith("_") and not k.startswith("__")}}
+for k in alive:
+    setattr(ops, k, None)
+del t
+import gc; gc.collect()
+print("ok" if not seen else seen)
+"""
+
+
+def _teardown_stdout(dev, real, dtype):
+    code = _TEARDOWN_SCRIPT.format(pkg=os.path.join(REPO, "velocity-asr_amd"), dev=dev, real=real, dtype=dtype)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+def test_weight_caches_exit_quietly():
+    """the weight caches' weakref callbacks looked their dict up as a module
+    global, which is None once interpreter teardown has cleared the module, and printed
+    AttributeError tracebacks at exit.  They now hold the dict itself (ops._dropper)."""
+    assert _teardown_stdout("cpu", False, "torch.bfloat16") == "ok"
+
+
+@pytest.mark.gpu
+def test_split_planes_exit_quietly():
+    assert _teardown_stdout("cuda", True, "torch.float32") == "ok"

@@ -79,13 +79,19 @@ __device__ __forceinline__ void collapse_wave(const int32_t* p, int L, int ldL, 
     }
 }
 
+// Rows utterance b collapses: frames[b] clamped to [0, L] (a value past L would read predictions
+// this launch did not write and write tokens past the utterance's row), or all L.
+__device__ __forceinline__ int frames_of(const int32_t* frames, int b, int ldL) {
+    return frames ? min(max(frames[b], 0), ldL) : ldL;
+}
+
 // frames (optional): utterance b collapses its own first frames[b] rows (row stride stays L).
 __global__ __launch_bounds__(64) void collapse_kernel(const int32_t* __restrict__ pred, int ldL, int blank, int collapse,
                                                       int32_t* __restrict__ toks, int32_t* __restrict__ lens,
                                                       int32_t* __restrict__ st, int32_t* __restrict__ en,
                                                       const int32_t* __restrict__ frames) {
     const int b = blockIdx.x;
-    collapse_wave(pred + (int64_t)b * ldL, frames ? frames[b] : ldL, ldL, b, blank, collapse, toks, lens, st, en);
+    collapse_wave(pred + (int64_t)b * ldL, frames_of(frames, b, ldL), ldL, b, blank, collapse, toks, lens, st, en);
 }
 
 // Argmax keys -> tokens -> collapse in one launch, one workgroup per utterance: its 256 threads
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(256) void collapse_keys_kernel(const unsigned long 
         if (pred) pred[(int64_t)b * ldL + t] = tok;
     }
     __syncthreads();
-    if (threadIdx.x < 64) collapse_wave(sp, frames ? frames[b] : ldL, ldL, b, blank, collapse, toks, lens, st, en);
+    if (threadIdx.x < 64) collapse_wave(sp, frames_of(frames, b, ldL), ldL, b, blank, collapse, toks, lens, st, en);
 }
 
 // One wave per two rows: lane l reads slot l % 32 of row 2w + l / 32 (coalesced), then a
@@ -169,7 +175,7 @@ VASR_API int vasr_ctc_collapse(const int32_t* pred, int B, int L, int blank, int
                         "vasr_ctc_collapse");
 }
 
-// frames (device): 0 <= frames[b] <= L rows of utterance b (row stride of pred and outputs stays L).
+// frames (device): frames[b] rows of utterance b, clamped to [0, L] (row stride of pred and outputs stays L).
 VASR_API int vasr_ctc_collapse_var(const int32_t* pred, int B, int L, const int32_t* frames, int blank, int collapse,
                                    int32_t* out_tokens, int32_t* out_len, int32_t* out_start, int32_t* out_end,
                                    void* stream) {

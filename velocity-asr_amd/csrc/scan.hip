@@ -49,6 +49,13 @@ VASR_API int64_t vasr_ssm_scan_workspace_floats(int B, int L, int Di, int N) {
     return 4 * (int64_t)B * ((L + 15) / 16) * Di * N;  // two arrays of [B][2 * nchunks][Di][N]
 }
 
+VASR_API int vasr_ssm_scan_split_selected(int B, int L, int Di, int N) {
+    using namespace vasr;
+    const int split_opt = option(VASR_OPT_SCAN_SPLIT);
+    const bool split_ok = N <= 64 && N > 0 && option(VASR_OPT_SCAN_LANES) != 4;
+    return split_ok && (split_opt == 2 || (split_opt == 0 && (int64_t)B * Di * N / 128 <= 256 && L <= 512)) ? 1 : 0;
+}
+
 VASR_API int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,
                                        const float* bc, int64_t ld_bc, const float* A2, const float* D, float* out,
                                        int64_t ld_out, int B, int L, int Di, int N, int mode, float* workspace,
@@ -82,9 +89,7 @@ VASR_API int vasr_ssm_scan_chunked_f32(const float* xz, int64_t ld_xz, const flo
     // slower from L ~ 1000 (one-utterance 30 s: 0.806 vs 0.777 ms; profiles/r05ap).
     // vasr_set_option(VASR_OPT_SCAN_SPLIT, 1|2) (env VASR_SCAN_SPLIT) forces them (three | one).
     // A forced 4-states-per-lane layout takes the three launches.
-    const int split_opt = option(VASR_OPT_SCAN_SPLIT);
-    const bool split_ok = N <= 64 && option(VASR_OPT_SCAN_LANES) != 4;
-    if (split_ok && (split_opt == 2 || (split_opt == 0 && (int64_t)B * Di * N / 128 <= 256 && L <= 512))) {
+    if (vasr_ssm_scan_split_selected(B, L, Di, N)) {
         switch (N) {
             case 16: return scan_split_n16(mode, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
             case 32: return scan_split_n32(mode, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);

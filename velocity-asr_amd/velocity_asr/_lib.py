@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -64,6 +64,7 @@ _SIGNATURES = {
     "vasr_ssm_scan_chunked_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5
                                   + [c_p, c_i64, c_p], ctypes.c_int),
     "vasr_ssm_scan_workspace_floats": ([ctypes.c_int] * 4, c_i64),
+    "vasr_ssm_scan_split_selected": ([ctypes.c_int] * 4, ctypes.c_int),
     "vasr_ssm_block_tail_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                 + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_ssm_block_tail_bf16": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]

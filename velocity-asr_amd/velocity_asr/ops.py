@@ -78,6 +78,15 @@ def _cuda_w(name: str, t: torch.Tensor) -> None:
     _cuda_f32(name, t)
 
 
+def _dropper(cache: dict, key: int):
+    """Weakref callback that drops `key` from `cache`.  The dict is bound into the closure (not
+    looked up as a module global): at interpreter exit the module's globals are cleared before
+    the last tensors die, and a global lookup then raised inside the callback."""
+    def drop(_ref, cache=cache, key=key):
+        cache.pop(key, None)
+    return drop
+
+
 # fp32 copies of bf16 parameters for the kernels that take fp32 operands (norm weights, biases,
 # conv taps, D, tables): built once per (tensor, version), dropped with the tensor.
 _f32_copies = {}
@@ -94,7 +103,7 @@ def f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     with torch.no_grad():
         c = t.detach().float().contiguous()
     key = id(t)
-    _f32_copies[key] = (weakref.ref(t, lambda _r, k=key: _f32_copies.pop(k, None)), sig, c)
+    _f32_copies[key] = (weakref.ref(t, _dropper(_f32_copies, key)), sig, c)
     return c
 
 
@@ -142,7 +151,7 @@ def split_weights(w: torch.Tensor) -> torch.Tensor:
     check(L.lib().vasr_split_weights_bf16x3(w.data_ptr(), ldw, N, K, planes.data_ptr(), stream_of(w)),
           "vasr_split_weights_bf16x3")
     key = id(w)
-    _splits[key] = (weakref.ref(w, lambda _r, k=key: _splits.pop(k, None)), sig, planes)
+    _splits[key] = (weakref.ref(w, _dropper(_splits, key)), sig, planes)
     return planes
 
 
@@ -161,7 +170,7 @@ def split_weights16(w: torch.Tensor) -> torch.Tensor:
     check(L.lib().vasr_split_weights16_bf16x3(w.data_ptr(), ldw, N, K, planes.data_ptr(), stream_of(w)),
           "vasr_split_weights16_bf16x3")
     key = id(w)
-    _splits16[key] = (weakref.ref(w, lambda _r, k=key: _splits16.pop(k, None)), sig, planes)
+    _splits16[key] = (weakref.ref(w, _dropper(_splits16, key)), sig, planes)
     return planes
 
 
@@ -177,7 +186,7 @@ def pack_weights16(w: torch.Tensor) -> torch.Tensor:
     check(L.lib().vasr_pack_weights16_bf16(w.data_ptr(), ldw, N, K, packed.data_ptr(), stream_of(w)),
           "vasr_pack_weights16_bf16")
     key = id(w)
-    _splits16[key] = (weakref.ref(w, lambda _r, k=key: _splits16.pop(k, None)), sig, packed)
+    _splits16[key] = (weakref.ref(w, _dropper(_splits16, key)), sig, packed)
     return packed
 
 
@@ -224,7 +233,7 @@ def pack_bf16(w: torch.Tensor) -> torch.Tensor:
     check(L.lib().vasr_pack_weights_bf16(w.data_ptr(), ldw, N, K, packed.data_ptr(), stream_of(w)),
           "vasr_pack_weights_bf16")
     key = id(w)
-    _splits[key] = (weakref.ref(w, lambda _r, k=key: _splits.pop(k, None)), sig, packed)
+    _splits[key] = (weakref.ref(w, _dropper(_splits, key)), sig, packed)
     return packed
 
 
@@ -432,11 +441,11 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
 # blocks' L = 64 at 10 s: 10.2 vs 6.8 us).
 # scan_form("streaming" | "chunked" | None) forces one (default from VASR_SCAN_CHUNKED=0|1).
 # Below CHUNKED_MIN_L the chunked entry point still wins where it runs as ONE launch (the
-# time-split form: N <= 64, B * Di * N / 128 <= 256 workgroups, L <= 512; include/vasr.h), e.g.
-# the global blocks' L = 64 at B = 1 (VASR_SCAN_SPLIT_SHORT=0 turns this off; profiles/r05aq).
+# time-split form: N <= 64, B * Di * N / 128 <= 256 workgroups, L <= 512; the library reports its
+# own rule, vasr_ssm_scan_split_selected), e.g. the global blocks' L = 64 at B = 1
+# (VASR_SCAN_SPLIT_SHORT=0 turns this off; profiles/r05aq).
 CHUNKED_MAX_WAVES = 256
 CHUNKED_MIN_L = 160
-SPLIT_MAX_L = 512
 _SCAN_FORM = {"0": "streaming", "1": "chunked"}.get(os.environ.get("VASR_SCAN_CHUNKED", ""))
 _SPLIT_SHORT = os.environ.get("VASR_SCAN_SPLIT_SHORT", "1") != "0"
 
@@ -462,10 +471,9 @@ def _use_chunked(B: int, Lq: int, Di: int, N: int, mode: int) -> bool:
 
 
 def _split_form(B: int, Lq: int, Di: int, N: int) -> bool:
-    """vasr_ssm_scan_chunked_f32 runs this launch as one (the time-split form) under the default
-    options (scan.hip's rule)."""
-    return (N <= 64 and B * Di * N // 128 <= 256 and Lq <= SPLIT_MAX_L
-            and L.lib().vasr_set_option(L.OPT_SCAN_SPLIT, -1) != 1 and L.lib().vasr_set_option(L.OPT_SCAN_LANES, -1) != 4)
+    """vasr_ssm_scan_chunked_f32 runs this launch as one (the time-split form) under the current
+    options: the library's own rule (vasr_ssm_scan_split_selected), not a copy of it."""
+    return bool(L.lib().vasr_ssm_scan_split_selected(B, Lq, Di, N))
 
 
 SCAN_STATE_DIMS = (16, 32, 64, 128)  # the scan kernels' state dims (include/vasr.h)

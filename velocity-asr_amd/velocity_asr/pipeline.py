@@ -190,7 +190,7 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
                           candidates: Optional[List[int]] = None, reps: int = 5, rounds: int = 3,
                           audio: Optional[torch.Tensor] = None,
                           agree: Optional[Callable[[Dict[int, float]], Dict[int, float]]] = None,
-                          max_rounds: int = 12, settle: float = 0.01):
+                          max_rounds: int = 12, settle: float = 0.01, keep_candidates: bool = False):
     """The GraphedTranscriber schedule that runs fastest on this device.
 
     One graph of the whole batch and two utterance-group graphs on concurrent streams give
@@ -201,10 +201,11 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
     is within `settle` of its previous one (at most `max_rounds`): a device fresh from idle runs
     the same replays up to 25 % slower for its first few tens of milliseconds of load
     (profiles/r05h/), so early rounds would time the ramp, not the schedule.  The fastest
-    candidate is returned; the others are kept alive on it until release_candidates() (freeing a
-    graph's memory pool stalls the device, which would idle it between the tuning and the caller's
-    first steps).  Returns (transcriber, {streams: best ms per replay}); the transcriber's
-    .autotune_rounds holds every round's times.
+    candidate is returned and the others are freed before returning, unless keep_candidates:
+    then they stay alive on the returned transcriber (their graphs and static buffers) until its
+    release_candidates() -- bench.py's choice, since freeing a graph's memory pool stalls the
+    device, which would idle it between the tuning and the timed steps.  Returns (transcriber,
+    {streams: best ms per replay}); the transcriber's .autotune_rounds holds every round's times.
 
     audio: the (batch, samples) clips the transcriber will serve, copied into every candidate
     before timing (the step's time depends on the data: the projection's per-chunk softplus
@@ -243,5 +244,7 @@ def autotuned_transcriber(model: VELOCITYASR, batch: int, samples: int, device: 
     best = min(cands, key=lambda s: times[s])
     keep = trs.pop(best)
     keep._candidates = list(trs.values())  # released by release_candidates()
+    if not keep_candidates:
+        keep.release_candidates()
     keep.autotune_rounds = [{s: round(t, 4) for s, t in h.items()} for h in hist]
     return keep, {s: round(t, 4) for s, t in times.items()}
