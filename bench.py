@@ -156,15 +156,18 @@ def kernel_roofline(model, audio, steps, streams=1):
                 main.wait_stream(st)
     rec = kt.summary()
     out = {}
-    # selective scan of the 8 local blocks (N=64): bytes = B*L*(4*Di + 2*N)*4 per launch
+    # selective scan of the 8 local blocks (N=64): bytes = B*L*(4*Di + 2*N)*4 per launch (x, z, dt
+    # and the output per channel, B and C per state); the ungated scan of the z-in-tail block reads
+    # no z: B*L*(3*Di + 2*N)*4
     scans = [(dt, i) for dt, i in rec["ssm_scan"] if i["N"] == model.config.ssm_state_dim]
     if scans:
         i = scans[0][1]
-        bytes_per = i["B"] * i["L"] * (4 * i["Di"] + 2 * i["N"]) * 4
+        bytes_per = i["B"] * i["L"] * ((3 if i.get("ungated") else 4) * i["Di"] + 2 * i["N"]) * 4
         elems = i["B"] * i["L"] * i["Di"] * i["N"]
         t = float(np.mean([d for d, _ in scans]))
         out["scan"] = dict(t=t, bytes=bytes_per, elems=elems, launches=len(scans), per_step=len(scans) / steps,
-                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"], N=i["N"], L=i["L"])
+                           total=sum(d for d, _ in scans) / steps, B=i["B"], Di=i["Di"], N=i["N"], L=i["L"],
+                           ungated=bool(i.get("ungated")))
     g = rec["gemm"]
     flops = [2.0 * i["M"] * i["N"] * i["K"] * i["batch"] for _, i in g]
     groups = {}
@@ -206,12 +209,35 @@ def isolated_times(model, audio, reps=20):
         blk = model.local_ssm.layers[0]
         u = ops.ln_dwconv(x, blk.norm1.weight, blk.norm1.bias, ops.f32(blk.conv.weight).view(D, -1),
                           blk.conv.bias, blk.norm1.eps).view(B * L, D)
+        p = blk.ssm._prepared()
+        if blk._z_in_tail(B, L, D):  # the z-in-tail block: projection without z, ungated scan, gated tail
+            from velocity_asr import _lib
+            from velocity_asr.ssm import _tree_mode
+            Di, N = blk.ssm.d_inner, blk.ssm.state_dim
+            proj = lambda: ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM,  # noqa: E731
+                                    n_out=Di + 2 * N)
+            xbd = proj()
+            mode = _tree_mode()
+            out = dict(scan=per_launch(lambda: ops.ssm_scan_ungated(xbd[:, :Di], xbd[:, Di + 2 * N:],
+                                                                    xbd[:, Di:Di + 2 * N], p["A2"], blk.ssm.D, B, L,
+                                                                    mode)),
+                       scan_key=(B, L), gemm=per_launch(proj), gemm_key=(B * L, p["w_noz"].shape[0], D, 1))
+            yd = ops.ssm_scan_ungated(xbd[:, :Di], xbd[:, Di + 2 * N:], xbd[:, Di:Di + 2 * N], p["A2"], blk.ssm.D,
+                                      B, L, mode)
+            x2 = x.view(B * L, D)
+            out["tail"] = per_launch(lambda: ops.ssm_block_tail_gated(
+                yd, u, p["w_z"], mode, x2, blk.ssm.out_proj.weight, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps,
+                blk.ffn[0].weight, blk.ffn[0].bias, blk.ffn[3].weight, blk.ffn[3].bias))
+            return out
         xz, xdt = blk.ssm.project(u)
         out = dict(scan=per_launch(lambda: blk.ssm.scan(xz, xdt, B, L)), scan_key=(B, L))
-        p = blk.ssm._prepared()
         if "w_comb" in p:  # the composed projection: one GEMM (fp32 model)
             out["gemm"] = per_launch(lambda: blk.ssm.project(u))
             out["gemm_key"] = (B * L, p["w_comb"].shape[0], D, 1)
+        g = blk.ssm.scan(xz, xdt, B, L)
+        x2 = x.view(B * L, D)
+        if blk._fused_tail_ok(D):
+            out["tail"] = per_launch(lambda: blk.tail(g, x2, B, L))
     return out
 
 
@@ -732,7 +758,9 @@ def result_line(args, world, distributed, B, S_len, streams, schedule, elapsed, 
         if iso.get("scan_key") == (sc["B"], sc["L"]):
             s_t, s_src = iso["scan"], "isolated: 20 back-to-back launches on the bench's operands, one HIP event pair"
         ach = sc["bytes"] / s_t / 1e9
-        roof = dict(bound="hbm", kernel="vasr ssm_scan (tree scan + gate, 8 local blocks, B*L*(4*Di+2*N)*4 B/launch)",
+        roof = dict(bound="hbm", kernel=("vasr ssm_scan_ungated (tree scan + x D, z-in-tail blocks, 8 local blocks, "
+                                         "B*L*(3*Di+2*N)*4 B/launch)" if sc.get("ungated") else
+                                         "vasr ssm_scan (tree scan + gate, 8 local blocks, B*L*(4*Di+2*N)*4 B/launch)"),
                     achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                     traffic=None, avg_launch_us=round(s_t * 1e6, 2), time_source=s_src,
                     insitu_avg_launch_us=round(sc["t"] * 1e6, 2))
@@ -795,6 +823,8 @@ def result_line(args, world, distributed, B, S_len, streams, schedule, elapsed, 
                                              gelem_per_s=round(sc["elems"] / sc["t"] / 1e9, 1)),
             "gemm": dict(avg_launch_us=round(gm["t"] * 1e6, 2), launches_per_step=gm["per_step"],
                          ms_per_step=round(gm["total"] * 1e3, 3), tflops=round(gm["tflops"], 2)),
+            "ssm_tail_isolated_us": round(iso["tail"] * 1e6, 2) if "tail" in iso else None,
+            "z_in_tail": bool(sc and sc.get("ungated")),
         },
         "token_checksum": [int(csum[0].item()), int(csum[1].item())],
         "graph_tokens_match_eager": graph_match,

@@ -184,6 +184,16 @@ int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t l
                       float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
                       void* stream);
 
+/* The ungated form of the tree modes (0, 2) for the z-in-tail SSMBlock (ABI 15):
+ *   out[b,t,d] = sum_n h[b,t,d,n] C[b,t,n] + x[b,t,d] D[d]
+ * with x = x[:, :, 0:Di] (row stride ld_x >= Di; no z is read) and the other operands as
+ * vasr_ssm_scan_f32; the same kernels and lane layout, so out * silu(z) (gate.h) is bitwise
+ * vasr_ssm_scan_f32's output.  vasr_ssm_block_tail_gated_f32 applies the gate. */
+int vasr_ssm_scan_ungated_f32(const float* x, int64_t ld_x, const float* dt, int64_t ld_dt,
+                              const float* bc, int64_t ld_bc, const float* A2, const float* D,
+                              float* out, int64_t ld_out, int B, int L, int Di, int N, int mode,
+                              void* stream);
+
 /* Chunk-parallel form of modes 0 and 2 for small launches (one utterance at a time, as
  * scripts/transcribe.py:69-78 and evaluate.py:91-98 run the model): time is cut at the
  * streaming kernel's 16-step chunks; pass 1 forms each chunk's up-sweep composite, pass 2
@@ -218,6 +228,17 @@ int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x, int64_t
                             const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
                             const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
                             int M, int D, int E, void* stream);
+/* The tail of the z-in-tail block (ABI 15): z = u @ W_z^T (W_z = in_proj rows Di..2Di-1 as
+ * vasr_split_weights_bf16x3 planes; u (M, D) the in_proj input, row stride ldu) with the split
+ * GEMM's exact product, g = yd * silu(z) with the gate of scan mode `mode` (0 or 2; yd = the
+ * vasr_ssm_scan_ungated_f32 output, row stride ldy), then the tail above on g.  Bitwise the
+ * output of vasr_ssm_scan_f32 + vasr_ssm_block_tail_f32 on the full projection; the projection
+ * GEMM no longer writes z (E floats per token).  32-row workgroups of 12 waves. */
+int vasr_ssm_block_tail_gated_f32(const float* yd, int64_t ldy, const float* u, int64_t ldu, const uint16_t* wz,
+                                  int mode, const float* x, int64_t ldx, const uint16_t* wo16,
+                                  const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                                  const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
+                                  int M, int D, int E, void* stream);
 /* The same tail for the bf16 model (C3): weights as one bf16 plane (vasr_pack_weights16_bf16 of
  * the bf16 parameters), activations rounded to bf16 at the MFMA input, fp32 accumulation and
  * fp32 LayerNorm / bias / GELU / residual -- the arithmetic of vasr_linear_bf16. */

@@ -503,6 +503,51 @@ def gen_c4full():
     save("fwd_fullbatch.npz", **out)
 
 
+TIE_MARGIN = 2e-5  # near-ties: reference top-2 margins below this (> 2x the largest |dlogit| measured)
+
+
+def _logits_pack(prefix, model, audio, chunk, every, out, check_tokens=None):
+    """Reference logits at the headline shapes (VERDICT r05, next 2): frames 0::every of every
+    clip (all 1000 classes), plus the full rows of every near-tie frame (reference top-2 margin
+    < TIE_MARGIN) with their (clip, frame) indices; the argmax tokens must equal the earlier
+    tokens-only golden of the same chunking."""
+    subs, ties_idx, ties_rows, toks = [], [], [], []
+    for i in range(0, audio.shape[0], chunk):
+        with torch.no_grad():
+            mel = ref_audio.compute_mel_spectrogram(torch.from_numpy(audio[i:i + chunk]))
+            logits = model(mel)
+        subs.append(logits[:, ::every].numpy())
+        top2 = torch.topk(logits, 2, dim=-1).values
+        m = (top2[..., 0] - top2[..., 1]).numpy()
+        for b, f in np.argwhere(m < TIE_MARGIN):
+            ties_idx.append((i + int(b), int(f)))
+            ties_rows.append(logits[b, f].numpy())
+        toks.append(logits.argmax(-1).numpy().astype(np.int16))
+        print(f"  {prefix}: clips {i}..{i + chunk - 1} done", flush=True)
+    toks = np.concatenate(toks)
+    if check_tokens is not None and not np.array_equal(toks, check_tokens):
+        raise AssertionError(f"{prefix}: argmax tokens differ from the tokens-only golden")
+    out[prefix + "every"] = np.array(every, np.int32)
+    out[prefix + "logits_sub"] = np.concatenate(subs).astype(np.float32)
+    out[prefix + "tie_idx"] = np.array(ties_idx, np.int32).reshape(-1, 2)
+    out[prefix + "tie_logits"] = np.array(ties_rows, np.float32).reshape(-1, out[prefix + "logits_sub"].shape[-1])
+
+
+def gen_headline_logits():
+    """fwd_headline_logits.npz: logits for all 32 clips of C2 (32 x 10 s, frames 0::25, reference
+    in chunks of 8) and C4 (32 x 30 s, frames 0::75, chunks of 4) -- the same chunkings as
+    fwd_fullbatch.npz, whose tokens they must reproduce -- and every near-tie frame's full row."""
+    model = build_model()
+    full = np.load(os.path.join(HERE, "fwd_fullbatch.npz"), allow_pickle=False)
+    out = {}
+    _logits_pack("c2_", model, syn.make_audio(32, 160000, seed=1234), 8, 25, out, full["c2_tokens"])
+    _logits_pack("c4_", model, syn.make_audio(32, 480000, seed=1234), 4, 75, out, full["c4_tokens"])
+    out["meta"] = meta(c2="make_audio(32, 160000, seed=1234), reference run in chunks of 8, frames 0::25",
+                       c4="make_audio(32, 480000, seed=1234), reference run in chunks of 4, frames 0::75",
+                       tie_margin=TIE_MARGIN, weights="make_weights(None, seed=0)")
+    save("fwd_headline_logits.npz", **out)
+
+
 def _greedy_pack(prefix, model, audio, chunk, out, decoded, cast=None):
     """Like _tokens_pack for a model whose forward takes `cast(mel)` (bf16): argmax tokens and
     greedy lists only (margins are meaningless for the statistical configs)."""
@@ -636,6 +681,8 @@ if __name__ == "__main__":
         gen_fullbatch()
     if "c4full" in which:  # ~4 min on 8 threads: not in the default list
         gen_c4full()
+    if "headline" in which:  # ~3 min on 8 threads: not in the default list
+        gen_headline_logits()
     if "benchsets" in which:  # long (~30 min on 8 threads): not in the default list
         gen_benchsets()
     if "statedims" in which:

@@ -624,6 +624,47 @@ def test_full_batch_30s_pinned(va, model):
     assert token_lists(*audio_to_token_ids(model, audio)) == json.loads(str(g["greedy"]))["c4"]
 
 
+HEADLINE_TOL = dict(atol=1e-4, rtol=1e-5)  # the fp tolerance of SURVEY §8 d, at the headline shapes
+
+
+@pytest.mark.parametrize("fma", ["1", "0"], ids=["mode2", "mode0"])
+@pytest.mark.parametrize("cfg,secs", [("c2", 10), ("c4", 30)])
+def test_headline_logits_pinned(va, model, monkeypatch, cfg, secs, fma):
+    """logits, not only tokens, pinned at C2 (32 x 10 s) and C4 (32 x 30 s),
+    each as ONE B = 32 forward: every clip's frames 0::every (all 1000 classes) within atol 1e-4
+    / rtol 1e-5 of the reference's (tests/golden/fwd_headline_logits.npz, the reference run in
+    chunks of 8 / 4), in both scan modes (2: the default fused multiply-adds; 0: the reference
+    tree op for op).  Every near-tie frame (reference top-2 margin < 2e-5, > 2x the largest
+    |dlogit| measured) is compared in full and its top-1 must be the reference's."""
+    monkeypatch.setenv("VASR_SCAN_FMA", fma)
+    g = golden("fwd_headline_logits.npz")
+    audio = t(S.make_audio(32, secs * 16000, seed=1234))
+    with torch.no_grad():
+        logits = model(va.compute_mel_spectrogram(audio))
+    every = int(g[cfg + "_every"])
+    got = logits[:, ::every].cpu().numpy()
+    want = g[cfg + "_logits_sub"]
+    assert got.shape == want.shape
+    assert_logits(got, want, HEADLINE_TOL)
+    ties = g[cfg + "_tie_idx"]
+    if len(ties):
+        rows = logits[torch.from_numpy(ties[:, 0]).long().to(DEV), torch.from_numpy(ties[:, 1]).long().to(DEV)]
+        rows = rows.cpu().numpy()
+        ref_rows = g[cfg + "_tie_logits"]
+        assert_logits(rows, ref_rows, HEADLINE_TOL)
+        top = rows.argmax(-1)
+        ref_top = ref_rows.argmax(-1)
+        bad = [(int(b), int(f)) for (b, f), x, y in zip(ties, top, ref_top) if x != y]
+        assert not bad, f"{cfg}: near-tie frames whose top-1 differs from the reference: {bad}"
+        d = np.abs(rows - ref_rows).max(-1)
+        srt = np.sort(ref_rows, -1)
+        margins = srt[:, -1] - srt[:, -2]
+        from conftest import record_metric
+        record_metric(f"{cfg}_near_ties", mode=fma, count=int(len(ties)), min_margin=float(margins.min()),
+                      max_abs_dlogit_at_ties=float(d.max()), max_abs_dlogit_sub=float(np.abs(got - want).max()),
+                      ties_below_max_dlogit=int((margins < float(np.abs(got - want).max())).sum()))
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 64, 192), (33, 1280, 192), (501, 1280, 192), (8016, 1280, 192), (16032, 1280, 192),
                                    (300, 1000, 192), (129, 96, 128), (77, 200, 100), (1024, 192, 192)])
 @pytest.mark.parametrize("epi", ["none", "gelu", "softplus", "residual", "argmax"])

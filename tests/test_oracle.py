@@ -238,3 +238,23 @@ def test_scan_state_dims(case):
     A = (-np.exp(A_log)).astype(np.float32)
     np.testing.assert_allclose(R.parallel_scan(x, dt, A, Bm, Cm, D), g[name + "__parallel"], atol=5e-5, rtol=5e-5)
     np.testing.assert_allclose(R.sequential_scan(x, dt, A, Bm, Cm, D), g[name + "__sequential"], atol=5e-5, rtol=5e-5)
+
+
+def test_headline_logits_fixture_is_consistent():
+    """fwd_headline_logits.npz (the reference's logits at C2 / C4) agrees with
+    the tokens-only golden of the same reference runs: the argmax of every stored frame is the
+    stored token, every near-tie row's margin is below the recorded threshold, and each near-tie
+    frame is one of fwd_fullbatch.npz's frames with that margin."""
+    g = golden("fwd_headline_logits.npz")
+    full = golden("fwd_fullbatch.npz")
+    thr = json.loads(str(g["meta"]))["tie_margin"]
+    for cfg in ("c2", "c4"):
+        every = int(g[cfg + "_every"])
+        sub = g[cfg + "_logits_sub"]
+        np.testing.assert_array_equal(sub.argmax(-1), full[cfg + "_tokens"][:, ::every].astype(np.int64))
+        ties, rows = g[cfg + "_tie_idx"], g[cfg + "_tie_logits"]
+        s = np.sort(rows, -1)
+        assert ((s[:, -1] - s[:, -2]) < thr).all()
+        np.testing.assert_array_equal(rows.argmax(-1), full[cfg + "_tokens"][ties[:, 0], ties[:, 1]])
+        np.testing.assert_allclose(s[:, -1] - s[:, -2], full[cfg + "_margin"][ties[:, 0], ties[:, 1]], rtol=0, atol=1e-9)
+        assert len(ties) == int((full[cfg + "_margin"] < thr).sum())

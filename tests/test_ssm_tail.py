@@ -123,3 +123,58 @@ def test_fused_block_bf16_model(monkeypatch):
     plain = blk(x)
     err = (fused - plain).abs()
     assert err.max().item() < 2e-2 and err.mean().item() < 1e-3, (err.max().item(), err.mean().item())
+
+
+def _block(i):
+    import velocity_asr as va
+    from velocity_asr import synthetic as S
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    m = m.to(DEV).eval()
+    return m, m.local_ssm.layers[i]
+
+
+@pytest.mark.parametrize("fma", ["1", "0"], ids=["mode2", "mode0"])
+@pytest.mark.parametrize("B,L", [(9, 501), (32, 501), (11, 1501), (17, 257), (5, 1000)])
+def test_z_in_tail_block_bitwise(monkeypatch, B, L, fma):
+    """The z-in-tail block (projection without the z columns, ungated scan, tail that forms z
+    with the split GEMM's exact product and applies the scan's gate) vs the three-launch block:
+    bitwise equal, both scan modes, 4- and 2-states-per-lane scan layouts ((5, 1000): 480 waves)."""
+    _, blk = _block(2)
+    x = torch.from_numpy(np.random.default_rng(B * L).standard_normal((B, L, 192)).astype(np.float32)).to(DEV)
+    monkeypatch.setenv("VASR_SCAN_FMA", fma)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "1")
+    assert blk._z_in_tail(B, L, 192)
+    a = blk(x)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "0")
+    assert not blk._z_in_tail(B, L, 192)
+    b = blk(x)
+    assert torch.equal(a, b), (a - b).abs().max().item()
+
+
+def test_z_in_tail_model_logits_bitwise(monkeypatch):
+    """C2's shape (32 x 10 s, one forward): the model's logits with and without z-in-tail are
+    bitwise equal; small launches (one utterance) keep the gated scan."""
+    import velocity_asr as va
+    from velocity_asr import synthetic as S
+    m, blk = _block(0)
+    assert not blk._z_in_tail(1, 501, 192)
+    mel = va.compute_mel_spectrogram(torch.from_numpy(S.make_audio(32, 160000, seed=1234)).to(DEV))
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "1")
+    a = m(mel)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "0")
+    b = m(mel)
+    assert torch.equal(a, b)
+
+
+def test_z_in_tail_argument_checks():
+    from velocity_asr import _lib
+    lib = _lib.lib()
+    x = torch.zeros(64, device=DEV)
+    p = x.data_ptr()
+    # mode 1 (recurrence) has no ungated form; a null u / wz is refused
+    assert lib.vasr_ssm_scan_ungated_f32(p, 384, p, 384, p, 128, p, p, p, 384, 1, 1, 384, 64, 1, None) == -1
+    assert lib.vasr_ssm_block_tail_gated_f32(p, 384, None, 192, p, 2, p, 192, p, p, p, 1e-5, p, p, p, p, p, 192,
+                                             1, 192, 384, None) == -1
+    assert b"u" in lib.vasr_last_error()

@@ -2,6 +2,19 @@
 // dispatch to the per-state-dim launchers (scan_n<N>.hip; kernels in scan_kernels.h).
 #include "scan_kernels.h"
 
+namespace vasr {
+namespace {
+// Lane layout of the streaming kernel (see vasr_ssm_scan_f32): 2 state indices per lane below 512
+// waves at 4 per lane, unless vasr_set_option(VASR_OPT_SCAN_LANES, 2|4) forces one.  Shared by the
+// gated and ungated entry points: the layouts differ in the order of the y = sum_n h C sums.
+bool streaming_two(int B, int Di, int N) {
+    const int npl_env = option(VASR_OPT_SCAN_LANES);  // vasr_set_option / env VASR_SCAN_NPL
+    const long waves4 = (long)B * Di * N / 256;
+    return npl_env == 2 || (npl_env != 4 && waves4 < 512);
+}
+}  // namespace
+}  // namespace vasr
+
 VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt, const float* bc,
                                int64_t ld_bc, const float* A2, const float* D, float* out, int64_t ld_out, int B,
                                int L, int Di, int N, int mode, void* stream) {
@@ -27,9 +40,7 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
     // C2 +1.3 %, C3 (bf16) -2.6 %, C4 (30 s) -8.5 % (profiles/r02_npl/).  So 2 per lane is kept
     // for launches under half a wave per SIMD (B <= 4 at Di 384, N 64: 62 vs 69 us), where the
     // shorter serial chain per wave wins.  vasr_set_option(VASR_OPT_SCAN_LANES, 2|4) (env VASR_SCAN_NPL) forces one.
-    const int npl_env = option(VASR_OPT_SCAN_LANES);  // vasr_set_option / env VASR_SCAN_NPL
-    const long waves4 = (long)B * Di * N / 256;
-    const bool two = npl_env == 2 || (npl_env != 4 && waves4 < 512);
+    const bool two = streaming_two(B, Di, N);
 #define VASR_SCAN_N(NN) scan_streaming_n##NN(two, mode, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
     switch (N) {
         case 16: return VASR_SCAN_N(16);
@@ -42,6 +53,37 @@ VASR_API int vasr_ssm_scan_f32(const float* xz, int64_t ld_xz, const float* dt, 
             return VASR_EUNSUPPORTED;
     }
 #undef VASR_SCAN_N
+}
+
+VASR_API int vasr_ssm_scan_ungated_f32(const float* x, int64_t ld_x, const float* dt, int64_t ld_dt, const float* bc,
+                                       int64_t ld_bc, const float* A2, const float* D, float* out, int64_t ld_out, int B,
+                                       int L, int Di, int N, int mode, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && dt && bc && A2 && D && out, "vasr_ssm_scan_ungated_f32: null pointer");
+    VASR_CHECK_ARG(mode == 0 || mode == 2, "vasr_ssm_scan_ungated_f32: mode must be 0 or 2 (tree modes)");
+    VASR_CHECK_ARG(B >= 0 && L >= 0 && L <= 8192 && Di > 0, "vasr_ssm_scan_ungated_f32: bad shape B=%d L=%d Di=%d", B,
+                   L, Di);
+    VASR_CHECK_ARG(ld_x % 4 == 0 && ld_dt % 4 == 0 && ld_bc % 4 == 0 && Di % 4 == 0,
+                   "vasr_ssm_scan_ungated_f32: leading dims and Di must be multiples of 4");
+    VASR_CHECK_ARG(ld_x >= Di && ld_dt >= Di && ld_bc >= 2 * N && ld_out >= Di,
+                   "vasr_ssm_scan_ungated_f32: leading dims too small");
+    VASR_CHECK_ARG(((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dt) |
+                     reinterpret_cast<uintptr_t>(bc)) & 15) == 0,
+                   "vasr_ssm_scan_ungated_f32: inputs must be 16-byte aligned");
+    if (B == 0 || L == 0) return VASR_OK;
+    hipStream_t s = as_stream(stream);
+    const bool two = streaming_two(B, Di, N);
+#define VASR_SCAN_U(NN) scan_ungated_n##NN(two, mode, x, ld_x, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
+    switch (N) {
+        case 16: return VASR_SCAN_U(16);
+        case 32: return VASR_SCAN_U(32);
+        case 64: return VASR_SCAN_U(64);
+        case 128: return VASR_SCAN_U(128);
+        default:
+            set_error("vasr_ssm_scan_ungated_f32: state dim N=%d not supported (16, 32, 64, 128)", N);
+            return VASR_EUNSUPPORTED;
+    }
+#undef VASR_SCAN_U
 }
 
 VASR_API int64_t vasr_ssm_scan_workspace_floats(int B, int L, int Di, int N) {

@@ -35,6 +35,7 @@
 
 #include <type_traits>
 
+#include "gate.h"
 #include "vasr_internal.h"
 
 namespace vasr {
@@ -95,7 +96,6 @@ __device__ __forceinline__ f2 operator*(f2 a, f2 b) { return f2{a.x * b.x, a.y *
 __device__ __forceinline__ f2 operator+(f2 a, f2 b) { return f2{a.x + b.x, a.y + b.y}; }
 #endif
 
-constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr int T = 16;    // time steps per chunk (the chunk-parallel form; the streaming kernel's TC)
 constexpr int TP = T + 1;  // padded row of the per-channel partial-sum tile
 constexpr int NW = 4;    // waves per block
@@ -289,7 +289,10 @@ namespace vasr {
                              int64_t ld_out, int B, int L, int Di, hipStream_t s);                                  \
     int scan_chunked_n##NN(bool two, int mode, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,     \
                            const float* bc, int64_t ld_bc, const float* A2, const float* D, float* out,             \
-                           int64_t ld_out, int B, int L, int Di, float* ws_a, float* ws_b, hipStream_t s);
+                           int64_t ld_out, int B, int L, int Di, float* ws_a, float* ws_b, hipStream_t s);          \
+    int scan_ungated_n##NN(bool two, int mode, const float* x, int64_t ld_x, const float* dt, int64_t ld_dt,        \
+                           const float* bc, int64_t ld_bc, const float* A2, const float* D, float* out,             \
+                           int64_t ld_out, int B, int L, int Di, hipStream_t s);
 VASR_SCAN_LAUNCHERS(16)
 VASR_SCAN_LAUNCHERS(32)
 VASR_SCAN_LAUNCHERS(64)

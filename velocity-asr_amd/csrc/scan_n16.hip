@@ -5,11 +5,11 @@ namespace vasr {
 namespace {
 constexpr int N = 16;
 
-template <int M>
+template <int M, bool GATE = true>
 int streaming(bool two, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt, const float* bc, int64_t ld_bc,
               const float* A2, const float* D, float* out, int64_t ld_out, int B, int L, int Di, hipStream_t s) {
-    return two ? npl2::launch_n<N, M>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
-                   : npl4::launch_n<N, M>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
+    return two ? npl2::launch_n<N, M, GATE>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
+                   : npl4::launch_n<N, M, GATE>(xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
 }
 
 template <int M>
@@ -27,6 +27,14 @@ int scan_streaming_n16(bool two, int mode, const float* xz, int64_t ld_xz, const
     return mode == 0   ? streaming<0>(two, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
            : mode == 2 ? streaming<2>(two, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
                        : streaming<1>(two, xz, ld_xz, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
+}
+
+// the ungated form (tree modes): out = y + x D, z not read (the z-in-tail block)
+int scan_ungated_n16(bool two, int mode, const float* x, int64_t ld_x, const float* dt, int64_t ld_dt, const float* bc,
+                      int64_t ld_bc, const float* A2, const float* D, float* out, int64_t ld_out, int B, int L, int Di,
+                      hipStream_t s) {
+    return mode == 0 ? streaming<0, false>(two, x, ld_x, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s)
+                     : streaming<2, false>(two, x, ld_x, dt, ld_dt, bc, ld_bc, A2, D, out, ld_out, B, L, Di, s);
 }
 
 int scan_chunked_n16(bool two, int mode, const float* xz, int64_t ld_xz, const float* dt, int64_t ld_dt,

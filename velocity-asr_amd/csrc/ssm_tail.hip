@@ -32,6 +32,7 @@
 // there in between) + 36 KiB for the 192-wide planes of h.
 #include <cstdlib>
 
+#include "gate.h"
 #include "ssm_fused.h"
 
 namespace vasr {
@@ -315,6 +316,137 @@ __global__ __launch_bounds__(64 * (12 / CT), RT == 1 && CT == 3 ? 2 : 1) void ss
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The z-in-tail block: z = in_proj_z(u) is read only by the gate y * silu(z)
+// (ssm.py:106, :129), so the projection GEMM leaves its 384 z columns out (its C stores are what
+// bound it), the scan writes the ungated y + x D (vasr_ssm_scan_ungated_f32), and
+// this kernel forms z itself before the tail:
+//   z = u @ W_z^T      the rows / tile engines' exact product: per 32 x 32 chunk, 12 k-steps of
+//                      the same six v_mfma_f32_32x32x16_bf16 split products in the same order
+//                      (gemm_rows.hip), A = u split into its three planes, W_z in the
+//                      vasr_split_weights_bf16x3 layout -- so z is bitwise the projection's z;
+//   g = yD * silu(z)   the scan's gate (gate.h), into R's planes: bitwise the scan's g;
+// then the 36 steps of ssm_tail_kernel.  One workgroup = 32 rows x 12 waves (the form of
+// M > 4096): wave w owns z columns 32 w .. 32 w + 31, i.e. chunk w of W_z, all 32 rows.
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct GateParams {
+    const float* yd;      // (M, E) y + x D, row stride ldy
+    int64_t ldy;
+    const float* u;       // (M, D) the projection's input (ln_dwconv output), row stride ldu
+    int64_t ldu;
+    const uint16_t* wz;   // W_z = in_proj rows Di..2Di-1 as vasr_split_weights_bf16x3 planes
+};
+
+template <int MODE>
+__global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, GateParams G) {
+    using Ctx = TailCtx<3, 2, 1>;
+    constexpr int NT = 768;
+    constexpr int KSZ = TD / 16;  // z k-steps (16 k each)
+    __shared__ __attribute__((aligned(16))) char R[3 * Ctx::PE];
+    __shared__ __attribute__((aligned(16))) char H[3 * Ctx::PDB];
+    Ctx c{P, R, H};
+    c.lane = threadIdx.x & 63;
+    c.wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    c.r = c.lane & 15;
+    c.q = c.lane >> 4;
+    c.m0 = blockIdx.x * Ctx::ROWS;
+    const int zr = c.lane & 31, zh = c.lane >> 5;  // 32x32x16 operand map: row / column zr, k half zh
+    const int zcol = 32 * c.wave + zr;
+    // W_z fragments of k-steps 0 and 1 (chunk `wave` of the split layout: [KSZ][3][64 lanes][16 B])
+    const char* wzc = reinterpret_cast<const char*>(G.wz) + (int64_t)c.wave * KSZ * 3 * 1024 + c.lane * 16;
+    bf16x8 wf[3][3];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) wf[ks][pl] = *reinterpret_cast<const bf16x8*>(wzc + (ks * 3 + pl) * 1024);
+    // y + x D at this lane's z positions (rows (i & 3) + 8 (i >> 2) + 4 zh of the tile)
+    float yv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = c.m0 + (i & 3) + 8 * (i >> 2) + 4 * zh;
+        yv[i] = row < P.M ? G.yd[(int64_t)row * G.ldy + zcol] : 0.0f;
+    }
+    // u tile -> H's three planes (192-wide layout; rows past M repeat row M - 1, never stored)
+    {
+        static_assert(Ctx::ROWS * TD / 8 == NT, "one 8-float chunk of u per thread");
+        const int rr = threadIdx.x / (TD / 8), ch = threadIdx.x - rr * (TD / 8);
+        const float* src = G.u + (int64_t)min(c.m0 + rr, P.M - 1) * G.ldu + 8 * ch;
+        const float4 v0 = *reinterpret_cast<const float4*>(src);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        split_store8<3>(H, Ctx::PDB, rr * TD * 2 + ((ch ^ (rr & 7)) << 4), v0, v1);
+    }
+    lds_barrier();  // u planes complete
+    auto read_u = [&](int ks, bf16x8 (&a)[3]) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            a[pl] = *reinterpret_cast<const bf16x8*>(H + pl * Ctx::PDB + zr * TD * 2 + (((2 * ks + zh) ^ (zr & 7)) << 4));
+    };
+    bf16x8 af[2][3];
+    read_u(0, af[0]);
+    floatx16 zc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) zc[i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KSZ; ++ks) {
+        if (ks + 2 < KSZ) {
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                wf[(ks + 2) % 3][pl] = *reinterpret_cast<const bf16x8*>(wzc + ((ks + 2) * 3 + pl) * 1024);
+        }
+        if (ks + 1 < KSZ) read_u(ks + 1, af[(ks + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8(&a)[3] = af[ks & 1];
+        const bf16x8(&w)[3] = wf[ks % 3];
+        // gemm_rows.hip's order: small terms first, then the leading hi * hi term
+        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], w[0], zc, 0, 0, 0);
+        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[2], zc, 0, 0, 0);
+        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[1], zc, 0, 0, 0);
+        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[0], zc, 0, 0, 0);
+        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[1], zc, 0, 0, 0);
+        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[0], zc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // the first PD steps' weights of the tail's own stream, in flight during the gate
+    load_first<0, 3, 2, 1>(c);
+    // g = (y + x D) * silu(z) into R's planes; z + 0.0f as the projection's epilogue adds its
+    // zero bias to the z columns (the same sign of a zero)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int rl = (i & 3) + 8 * (i >> 2) + 4 * zh;
+        split_store<3>(R, Ctx::PE, poff<TE>(rl, zcol), yv[i] * silu_of<MODE>(zc[i] + 0.0f));
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+        const int col = 16 * c.wave + c.r;
+        c.bb2[0] = P.b2[col];
+        c.bb1[0][0] = P.b1[col];
+        c.bb1[1][0] = P.b1[TD + col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = c.m0 + 16 * tm + 4 * c.q + i;
+            c.x1[tm][0][i] = row < P.M ? P.x[(int64_t)row * P.ldx + col] : 0.0f;
+        }
+        c.acc[tm][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        c.lnw[i] = P.ln_w[c.lane + 64 * i];
+        c.lnb[i] = P.ln_b[c.lane + 64 * i];
+    }
+    lds_barrier();  // the g planes are complete (and every wave is past its u reads: H is free for h)
+    tail_step<0, 3, 2, 1>(c);
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm) {
+        const int col = 16 * c.wave + c.r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = c.m0 + 16 * tm + 4 * c.q + i;
+            if (row < P.M) P.out[(int64_t)row * P.ldo + col] = (c.acc[tm][0][i] + c.bb2[0]) + c.x1[tm][0][i];
+        }
+    }
+}
+
 // Fragment layout of v_mfma_f32_16x16x32_bf16's B operand, three split planes:
 // [ceil(N/16)][Kp/32][3][64 lanes][8], lane l of (tile nt, step ks) holding
 // W[16 nt + (l & 15)][32 ks + 8 (l >> 4) + j]; zero outside N x K.
@@ -474,4 +606,26 @@ VASR_API int vasr_ssm_block_tail_f32(const float* g, int64_t ldg, const float* x
     const TailParams p{g, ldg, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
     launch_tail<3>(p, as_stream(stream));
     return launch_status("vasr_ssm_block_tail_f32");
+}
+
+VASR_API int vasr_ssm_block_tail_gated_f32(const float* yd, int64_t ldy, const float* u, int64_t ldu, const uint16_t* wz,
+                                           int mode, const float* x, int64_t ldx, const uint16_t* wo16,
+                                           const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                                           const float* b1, const uint16_t* w2_16, const float* b2, float* out,
+                                           int64_t ldo, int M, int D, int E, void* stream) {
+    using namespace vasr;
+    if (int rc = tail_args(yd, ldy, x, ldx, wo16, ln_w, ln_b, w1_16, b1, w2_16, b2, out, ldo, M, D, E,
+                           "vasr_ssm_block_tail_gated_f32"))
+        return rc;
+    VASR_CHECK_ARG(u && wz && ldu >= D && ldu % 4 == 0 && (reinterpret_cast<uintptr_t>(u) & 15) == 0 &&
+                       (reinterpret_cast<uintptr_t>(wz) & 15) == 0,
+                   "vasr_ssm_block_tail_gated_f32: u (16-B aligned rows, ldu >= D, ldu %% 4 == 0) and wz needed");
+    VASR_CHECK_ARG(mode == 0 || mode == 2, "vasr_ssm_block_tail_gated_f32: mode must be 0 or 2 (the scan's gate)");
+    if (M == 0) return VASR_OK;
+    const TailParams p{yd, ldy, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
+    const GateParams gp{yd, ldy, u, ldu, wz};
+    const dim3 grid((unsigned)((M + 31) / 32)), block(768);
+    if (mode == 2) hipLaunchKernelGGL(ssm_tail_gated_kernel<2>, grid, block, 0, as_stream(stream), p, gp);
+    else hipLaunchKernelGGL(ssm_tail_gated_kernel<0>, grid, block, 0, as_stream(stream), p, gp);
+    return launch_status("vasr_ssm_block_tail_gated_f32");
 }

@@ -63,10 +63,14 @@ _SIGNATURES = {
                           ctypes.c_int),
     "vasr_ssm_scan_chunked_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5
                                   + [c_p, c_i64, c_p], ctypes.c_int),
+    "vasr_ssm_scan_ungated_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p],
+                                  ctypes.c_int),
     "vasr_ssm_scan_workspace_floats": ([ctypes.c_int] * 4, c_i64),
     "vasr_ssm_scan_split_selected": ([ctypes.c_int] * 4, ctypes.c_int),
     "vasr_ssm_block_tail_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                 + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
+    "vasr_ssm_block_tail_gated_f32": ([c_p, c_i64, c_p, c_i64, c_p, ctypes.c_int, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p,
+                                       c_p, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_ssm_block_tail_bf16": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                  + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_pack_weights16_bf16": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),

@@ -532,6 +532,63 @@ def ssm_scan(xz: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Ten
     return out
 
 
+def ssm_scan_ungated(x: torch.Tensor, dt: torch.Tensor, bc: torch.Tensor, A2: torch.Tensor, D: torch.Tensor, B: int,
+                     Lq: int, mode: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The ungated tree scan (vasr_ssm_scan_ungated_f32, modes 0 / 2): y + x D for x (B*L, Di),
+    dt (B*L, Di), bc (B*L, 2N) row views; no z.  The z-in-tail block's scan: the streaming
+    kernels with the gated entry point's lane layout, so ssm_block_tail_gated's gate gives
+    bitwise ssm_scan's output (the caller keeps to shapes where ssm_scan streams too)."""
+    D = f32(D)
+    for n, t in (("x", x), ("dt", dt), ("bc", bc), ("A2", A2), ("D", D)):
+        _cuda_f32(f"ssm_scan_ungated.{n}", t)
+    M, Di, ld_x = _rows("ssm_scan_ungated.x", x)
+    _, Di2, ld_dt = _rows("ssm_scan_ungated.dt", dt)
+    _, two_n, ld_bc = _rows("ssm_scan_ungated.bc", bc)
+    N = A2.numel()
+    if M != B * Lq or Di2 != Di or two_n != 2 * N or D.numel() != Di or N not in SCAN_STATE_DIMS:
+        raise ValueError("ssm_scan_ungated: inconsistent shapes")
+    if out is None:
+        out = torch.empty((M, Di), device=x.device, dtype=torch.float32)
+    _, _, ld_out = _rows("ssm_scan_ungated.out", out)
+    ev = _t0("ssm_scan")
+    check(L.lib().vasr_ssm_scan_ungated_f32(x.data_ptr(), ld_x, dt.data_ptr(), ld_dt, bc.data_ptr(), ld_bc,
+                                            A2.data_ptr(), D.data_ptr(), out.data_ptr(), ld_out, B, Lq, Di, N,
+                                            int(mode), stream_of(x)), "vasr_ssm_scan_ungated_f32")
+    _t1("ssm_scan", ev, dict(B=B, L=Lq, Di=Di, N=N, mode=int(mode), chunked=False, ungated=True))
+    return out
+
+
+def ssm_block_tail_gated(yd: torch.Tensor, u: torch.Tensor, wz: torch.Tensor, mode: int, x: torch.Tensor,
+                         wo: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, ln_eps: float, w1: torch.Tensor,
+                         b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The z-in-tail block's tail (vasr_ssm_block_tail_gated_f32): z = u W_z^T (the split GEMM's
+    exact product), g = yd * silu(z) (scan mode `mode`'s gate), then ssm_block_tail on g -- for
+    yd (M, 384) the ungated scan output, u (M, 192) the projection input, wz (384, 192) = in_proj
+    rows Di..2Di-1 (a persistent tensor: its split planes are cached by identity)."""
+    for n, t in (("yd", yd), ("u", u), ("wz", wz), ("x", x), ("ln_w", ln_w), ("ln_b", ln_b), ("b1", b1), ("b2", b2),
+                 ("wo", wo), ("w1", w1), ("w2", w2)):
+        _cuda_f32(f"ssm_block_tail_gated.{n}", t)
+    M, E, ldy = _rows("ssm_block_tail_gated.yd", yd)
+    Mu, D, ldu = _rows("ssm_block_tail_gated.u", u)
+    Mx, Dx, ldx = _rows("ssm_block_tail_gated.x", x)
+    if Mu != M or Mx != M or Dx != D or tuple(wz.shape) != (E, D) or tuple(wo.shape) != (D, E):
+        raise ValueError("ssm_block_tail_gated: inconsistent shapes")
+    if out is None:
+        out = torch.empty((M, D), device=yd.device, dtype=torch.float32)
+    _, _, ldo = _rows("ssm_block_tail_gated.out", out)
+    ev = _t0("ssm_tail")
+    check(L.lib().vasr_ssm_block_tail_gated_f32(yd.data_ptr(), ldy, u.data_ptr(), ldu, split_weights(wz).data_ptr(),
+                                                int(mode), x.data_ptr(), ldx, split_weights16(wo).data_ptr(),
+                                                ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(),
+                                                float(ln_eps), split_weights16(w1).data_ptr(),
+                                                b1.contiguous().data_ptr(), split_weights16(w2).data_ptr(),
+                                                b2.contiguous().data_ptr(), out.data_ptr(), ldo, M, D, E,
+                                                stream_of(yd)), "vasr_ssm_block_tail_gated_f32")
+    _t1("ssm_tail", ev, dict(M=M, D=D, E=E, gated=True))
+    return out
+
+
 def reflect_pad(audio: torch.Tensor, pad: int, ld_out: int) -> torch.Tensor:
     _cuda_f32("reflect_pad.audio", audio)
     audio = audio.contiguous()

@@ -99,6 +99,11 @@ class SelectiveSSM(nn.Module):
                 wc = (w.detach().double() @ self.in_proj.weight.detach()[:Di].double()).float()
                 out["w_comb"] = torch.cat([self.in_proj.weight.detach(), wc], 0).contiguous()
                 out["b_comb"] = torch.cat([torch.zeros(2 * Di, device=dev), b]).contiguous()
+                # the z-in-tail block (SSMBlock._z_in_tail): [x | B | C | dt] without the z rows, and
+                # W_z for the tail's own z product (the same rows, so the same split planes)
+                out["w_noz"] = torch.cat([self.in_proj.weight.detach()[:Di], wc], 0).contiguous()
+                out["b_noz"] = torch.cat([torch.zeros(Di, device=dev), b]).contiguous()
+                out["w_z"] = self.in_proj.weight.detach()[Di:].contiguous()
             return out
         return cached(self, "ssm", (self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, self.A_log,
                                     self.in_proj.weight), build)
@@ -178,9 +183,53 @@ class SSMBlock(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _check_eval(self)
         B, L, D = x.shape
+        if self._z_in_tail(B, L, D):
+            return self._forward_z_in_tail(x)
         x2, xz, xdt = self.head(x)
         g = self.ssm.scan(xz, xdt, B, L)
         return self.tail(g, x2, B, L)
+
+    # z-in-tail: z = in_proj_z(u) feeds only the gate y * silu(z)
+    # (ssm.py:106, :129).  The projection GEMM -- bound by its C stores -- then writes
+    # [x | B | C | dt] (896 of its 1280 columns), the scan writes the ungated y + x D, and the fused
+    # tail forms z itself with the split GEMM's exact product before applying the gate and the
+    # usual tail: bitwise the three-launch block's output (tests/test_ssm_tail.py).  Where it runs:
+    # the fp32 model with the composed projection, the tree scan streamed (ops._use_chunked false)
+    # and the 32-row tail (M > 4096 token rows: the bench's batches); VASR_Z_IN_TAIL=0 turns it off.
+    Z_IN_TAIL_MIN_ROWS = 4097
+
+    def _z_in_tail(self, B: int, L: int, D: int) -> bool:
+        ssm = self.ssm
+        if os.environ.get("VASR_Z_IN_TAIL", "1") == "0" or B * L < self.Z_IN_TAIL_MIN_ROWS:
+            return False
+        if _SCAN_MODE_ID[ssm.scan_mode] != 0 or os.environ.get("VASR_XDT_COMPOSE", "1") == "0":
+            return False
+        mods = (ssm.in_proj, ssm.x_proj, ssm.dt_proj, ssm.out_proj, self.ffn[0], self.ffn[3])
+        if not all(type(m) is nn.Linear and m.weight.dtype == torch.float32 for m in mods):
+            return False  # QAT (quantize.QuantizedLinear) and bf16 models keep the gated scan
+        if not self._fused_tail_ok(D):
+            return False
+        N = ops.scan_state_dim(ssm.state_dim)
+        if N != ssm.state_dim or ops._use_chunked(B, L, ssm.d_inner, N, _tree_mode()):
+            return False
+        return "w_noz" in ssm._prepared()
+
+    def _forward_z_in_tail(self, x: torch.Tensor) -> torch.Tensor:
+        B, L, D = x.shape
+        ssm = self.ssm
+        Di, N = ssm.d_inner, ssm.state_dim
+        p = ssm._prepared()
+        x = x.contiguous()
+        x2 = x.view(B * L, D)
+        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
+                          self.conv.bias, self.norm1.eps).view(B * L, D)
+        xbd = ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=Di + 2 * N)  # [x | B | C | dt]
+        mode = _tree_mode()
+        yd = ops.ssm_scan_ungated(xbd[:, :Di], xbd[:, Di + 2 * N:], xbd[:, Di:Di + 2 * N], p["A2"], ssm.D, B, L, mode)
+        out = ops.ssm_block_tail_gated(yd, u, p["w_z"], mode, x2, ssm.out_proj.weight, self.norm2.weight,
+                                       self.norm2.bias, self.norm2.eps, self.ffn[0].weight, self.ffn[0].bias,
+                                       self.ffn[3].weight, self.ffn[3].bias)
+        return out.view(B, L, D)
 
     # The block in three stages -- head (LN1, causal dwconv, projections), the scan, tail (out_proj
     # + residual, LN2, FFN + residual).  (Issuing one utterance group's scans on a stream of their
