@@ -32,10 +32,28 @@ def cases():
                         yield ("chunked", N, Di, B, L, mode, npl, 16)
 
 
+def _lib_direct():
+    """The library under test (VASR_LIB or the in-tree build) through ctypes alone, so libraries of
+    other ABI versions (e.g. the round-start build) dump the same cases: only the scan entry points
+    and vasr_set_option, whose signatures every ABI since 12 shares."""
+    import ctypes
+    path = os.environ.get("VASR_LIB") or os.path.join(REPO, "velocity-asr_amd", "velocity_asr", "lib", "libvasr_hip.so")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    c_p, c_i64, c_i = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    lib.vasr_ssm_scan_f32.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [c_i] * 5 + [c_p]
+    lib.vasr_ssm_scan_chunked_f32.argtypes = ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [c_i] * 5
+                                              + [c_p, c_i64, c_p])
+    lib.vasr_ssm_scan_workspace_floats.argtypes = [c_i] * 4
+    lib.vasr_ssm_scan_workspace_floats.restype = c_i64
+    lib.vasr_set_option.argtypes = [c_i, c_i]
+    lib.vasr_set_option.restype = c_i
+    return lib
+
+
 def dump(path):
     import torch
-    from velocity_asr import _lib, ops
-    _lib.load()
+    lib = _lib_direct()
+    OPT_SCAN_LANES, OPT_SCAN_CHUNK = 0, 1  # enum vasr_option (include/vasr.h)
     out = {}
     for form, N, Di, B, L, mode, npl, tc in cases():
         g = torch.Generator(device="cuda").manual_seed(1000 * N + 7 * L + B)
@@ -46,12 +64,22 @@ def dump(path):
         A2 = -(torch.arange(1, N + 1, device="cuda", dtype=torch.float32)
                + 0.1 * torch.rand(N, device="cuda", generator=g)) * 1.4426950408889634
         D = 1 + 0.1 * torch.randn(Di, device="cuda", generator=g)
-        prev = ops.scan_form(form)
+        y = torch.empty(M, Di, device="cuda")
+        p0 = lib.vasr_set_option(OPT_SCAN_LANES, npl)
+        p1 = lib.vasr_set_option(OPT_SCAN_CHUNK, tc)
+        args = (xz.data_ptr(), 2 * Di, dt.data_ptr(), Di, bc.data_ptr(), 2 * N, A2.data_ptr(), D.data_ptr(),
+                y.data_ptr(), Di, B, L, Di, N, mode)
         try:
-            with ops.option(_lib.OPT_SCAN_LANES, npl), ops.option(_lib.OPT_SCAN_CHUNK, tc):
-                y = ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode)
+            if form == "chunked":
+                nws = lib.vasr_ssm_scan_workspace_floats(B, L, Di, N)
+                ws = torch.empty(max(nws, 4), device="cuda")
+                rc = lib.vasr_ssm_scan_chunked_f32(*args, ws.data_ptr(), nws, None)
+            else:
+                rc = lib.vasr_ssm_scan_f32(*args, None)
         finally:
-            ops.scan_form(prev)
+            lib.vasr_set_option(OPT_SCAN_LANES, p0)
+            lib.vasr_set_option(OPT_SCAN_CHUNK, p1)
+        assert rc == 0, (form, N, Di, B, L, mode, npl, tc, rc)
         torch.cuda.synchronize()
         out["|".join(map(str, (form, N, Di, B, L, mode, npl, tc)))] = y.cpu().numpy()
     np.savez(path, **out)

@@ -338,6 +338,24 @@ struct GateParams {
     const uint16_t* wz;   // W_z = in_proj rows Di..2Di-1 as vasr_split_weights_bf16x3 planes
 };
 
+// g = y * silu(z) split into R's three planes, with contraction off for the product AND the split:
+// left to the default (fp-contract=fast) the compiler forms the split's residual g - hi as one fma
+// from the unrounded product, i.e. planes of a more exact g than the scan writes (1e-6 differences
+// at the block output; the scan TU is built with -ffp-contract=off).  z + 0.0f: the projection's
+// epilogue adds its zero bias to the z columns (the same sign of a zero).
+template <int MODE>
+__device__ __forceinline__ void gate_split_store(char* plane0, int plane_bytes, int off, float y, float z) {
+#pragma clang fp contract(off)
+    const float v = y * silu_of<MODE>(z + 0.0f);
+    const __bf16 hi = (__bf16)v;
+    const float r1 = v - (float)hi;
+    const __bf16 mid = (__bf16)r1;
+    const __bf16 lo = (__bf16)(r1 - (float)mid);
+    *reinterpret_cast<__bf16*>(plane0 + off) = hi;
+    *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = mid;
+    *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = lo;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, GateParams G) {
     using Ctx = TailCtx<3, 2, 1>;
@@ -409,12 +427,11 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
     }
     // the first PD steps' weights of the tail's own stream, in flight during the gate
     load_first<0, 3, 2, 1>(c);
-    // g = (y + x D) * silu(z) into R's planes; z + 0.0f as the projection's epilogue adds its
-    // zero bias to the z columns (the same sign of a zero)
+    // g = (y + x D) * silu(z) into R's planes
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int rl = (i & 3) + 8 * (i >> 2) + 4 * zh;
-        split_store<3>(R, Ctx::PE, poff<TE>(rl, zcol), yv[i] * silu_of<MODE>(zc[i] + 0.0f));
+        gate_split_store<MODE>(R, Ctx::PE, poff<TE>(rl, zcol), yv[i], zc[i]);
     }
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
