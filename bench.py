@@ -763,7 +763,13 @@ def result_line(args, world, distributed, B, S_len, streams, schedule, elapsed, 
                                          "vasr ssm_scan (tree scan + gate, 8 local blocks, B*L*(4*Di+2*N)*4 B/launch)"),
                     achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4),
                     traffic=None, avg_launch_us=round(s_t * 1e6, 2), time_source=s_src,
-                    insitu_avg_launch_us=round(sc["t"] * 1e6, 2))
+                    insitu_avg_launch_us=round(sc["t"] * 1e6, 2), algorithmic_bytes_per_launch=sc["bytes"])
+        if sc.get("ungated"):
+            # z-in-tail: the scan no longer reads z (Di floats per token), so its algorithmic bytes and
+            # its HBM fraction are smaller at the same state work; the gated scan's byte count at this
+            # launch time is given beside it for comparison with earlier lines (not the achieved rate)
+            gb = sc["B"] * sc["L"] * (4 * sc["Di"] + 2 * sc["N"]) * 4
+            roof.update(gated_bytes_per_launch=gb, frac_at_gated_bytes=round(gb / s_t / 1e9 / HBM_PEAK_GBS, 4))
         # the scan is VALU-bound: the same launch against the fp32 vector roof at the
         # reference tree's ~11 fp32 operations per state element (SURVEY §8 d), and the HBM fraction
         # that arithmetic allows at best: (bytes/elem / HBM peak) / (ops/elem / VALU peak)

@@ -33,9 +33,19 @@ def main():
         data[(B, L)] = (xz, dt, bc, A2, D, torch.empty(M, Di, device="cuda"))
     res = {}
     st = torch.cuda.current_stream().cuda_stream
+    # warm the chip up first (the clock ramps over the first ~2 s of load, profiles/r06d/l_clock.txt),
+    # then rotate the library order every round so no library always runs first or last
+    import time
+    (B0, L0), (xz, dt, bc, A2, D, out) = next(iter(data.items()))
+    t_end = time.time() + float(__import__("os").environ.get("AB_WARM_S", "3"))
+    while time.time() < t_end:
+        for _ in range(20):
+            fns[0][1](xz.data_ptr(), 2 * Di, dt.data_ptr(), Di, bc.data_ptr(), 2 * N, A2.data_ptr(), D.data_ptr(),
+                      out.data_ptr(), Di, B0, L0, Di, N, 2, st)
+        torch.cuda.synchronize()
     for r in range(rounds):
         for (B, L), (xz, dt, bc, A2, D, out) in data.items():
-            for name, f in fns:
+            for name, f in fns[r % len(fns):] + fns[:r % len(fns)]:
                 args = (xz.data_ptr(), 2 * Di, dt.data_ptr(), Di, bc.data_ptr(), 2 * N, A2.data_ptr(), D.data_ptr(),
                         out.data_ptr(), Di, B, L, Di, N, 2, st)
                 for _ in range(3):
@@ -47,7 +57,6 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 res.setdefault((B, L, name), []).append(s.elapsed_time(e) / reps * 1e3)
-                h = hash(out.view(torch.int32).sum().item())
                 res.setdefault((B, L, name, "digest"), set()).add(int(out.view(torch.int32).double().sum().item()))
     for k, v in res.items():
         if k[-1] == "digest":
