@@ -27,7 +27,10 @@ SPLIT = [("in_proj", 768, 192, "none", None), ("x_dt", 512, 384, "softplus", 768
          ("out_proj", 192, 384, "residual", None), ("ffn1", 384, 192, "gelu", None),
          ("ffn2", 192, 384, "residual", None), ("head_argmax", 1000, 192, "argmax", None)]
 HEAD = [("head_comp", 1280, 192, "softplus", None), ("ctc_argmax", 1000, 192, "argmax", None),
-        ("tail", 192, 384, "tail", None), ("tail_global", 192, 384, "tail1024", None)]
+        ("tail", 192, 384, "tail", None), ("tail_global", 192, 384, "tail1024", None),
+        # the z-in-tail block (round 6): the projection without z (softplus from column 512) and the
+        # tail that forms z itself (ssm_tail_gated_kernel: z product + the three tail products)
+        ("head_noz", 896, 192, "softplus", None), ("tail_gated", 192, 384, "tailg", None)]
 
 
 def main():
@@ -45,7 +48,23 @@ def main():
         rows = K == 192 and N >= 512 and m >= 4096 and epi in ("none", "gelu", "softplus")
         kernel = "gemm_rows_kernel" if rows else "gemm_x3_kernel"
         flops = 2.0 * m * N * K
-        if epi.startswith("tail"):
+        if epi == "tailg":
+            D, Ei = 192, 384
+            yd = torch.randn(m, Ei, device="cuda", generator=g)
+            u = torch.randn(m, D, device="cuda", generator=g)
+            wz = torch.randn(Ei, D, device="cuda", generator=g) / D ** 0.5
+            x = torch.randn(m, D, device="cuda", generator=g)
+            wo = torch.randn(D, Ei, device="cuda", generator=g) / Ei ** 0.5
+            w1 = torch.randn(Ei, D, device="cuda", generator=g) / D ** 0.5
+            w2 = torch.randn(D, Ei, device="cuda", generator=g) / Ei ** 0.5
+            lw, lb = torch.ones(D, device="cuda"), torch.zeros(D, device="cuda")
+            b1, b2 = torch.randn(Ei, device="cuda", generator=g), torch.randn(D, device="cuda", generator=g)
+
+            def fn():
+                return ops.ssm_block_tail_gated(yd, u, wz, 2, x, wo, lw, lb, 1e-5, w1, b1, w2, b2)
+            kernel = "ssm_tail_gated_kernel"
+            flops = 4 * 2.0 * m * D * Ei  # z, out_proj, ffn1, ffn2
+        elif epi.startswith("tail"):
             D, Ei = 192, 384
             gin = torch.randn(m, Ei, device="cuda", generator=g)
             x = torch.randn(m, D, device="cuda", generator=g)
@@ -65,7 +84,7 @@ def main():
             b = torch.randn(N, device="cuda", generator=g)
             kw = {}
             if epi == "softplus":
-                kw["n_out"] = 896 if name == "head_comp" else 128
+                kw["n_out"] = {"head_comp": 896, "head_noz": 512}.get(name, 128)
             if epi == "residual":
                 kw["aux"] = torch.randn(m, N, device="cuda", generator=g)
             if epi == "argmax":

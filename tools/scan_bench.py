@@ -25,8 +25,15 @@ def main():
     A2 = -torch.arange(1, N + 1, device="cuda", dtype=torch.float32) * 1.4426950408889634
     D = torch.ones(Di, device="cuda")
     out = torch.empty(M, Di, device="cuda")
+    ungated = os.environ.get("SCAN_UNGATED", "0") == "1"  # the z-in-tail block's scan (no z, no gate)
+
+    def run():
+        if ungated:
+            ops.ssm_scan_ungated(xz[:, :Di], dt, bc, A2, D, B, L, mode, out=out)
+        else:
+            ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode, out=out)
     for _ in range(5):
-        ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode, out=out)
+        run()
     torch.cuda.synchronize()
     # the launches replayed from a HIP graph: kernel time without the host wrapper's per-call cost
     st = torch.cuda.Stream()
@@ -34,7 +41,7 @@ def main():
     gr = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gr, stream=st):
         for _ in range(reps):
-            ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode, out=out)
+            run()
     gr.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,9 +50,9 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / reps * 1e3
-    byts = B * L * (4 * Di + 2 * N) * 4
+    byts = B * L * ((3 if ungated else 4) * Di + 2 * N) * 4
     form = sys.argv[7] if len(sys.argv) > 7 else "auto"
-    print(f"scan B={B} L={L} Di={Di} N={N} mode={mode} {form}: {us:.1f} us/launch, {byts / us / 1e3:.1f} GB/s, "
+    print(f"scan B={B} L={L} Di={Di} N={N} mode={mode} {form}{' ungated' if ungated else ''}: {us:.1f} us/launch, {byts / us / 1e3:.1f} GB/s, "
           f"{B * L * Di * N / us / 1e3:.1f} Gelem/s")
 
 

@@ -26,7 +26,7 @@ PEAK_BF16 = 2500e12
 PEAK_F32 = 157.3e12
 
 
-FAMILIES = ("gemm_x3_kernel", "gemm_rows_kernel", "ssm_tail_kernel")
+FAMILIES = ("gemm_x3_kernel", "gemm_rows_kernel", "ssm_tail_gated_kernel", "ssm_tail_kernel")
 
 
 def family_rows(path):
@@ -78,7 +78,8 @@ def main(tag, Ms):
                        mfma_tflops=round(mops / dur / 1e12, 1), mfma_frac=round(mops / dur / PEAK_BF16, 4),
                        busy_per_simd=round(busy), mfma_busy_frac=round(busy / (dur * CLOCK), 4),
                        f32eq_tflops=round(sh["flops"] / dur / 1e12, 2), f32eq_frac=round(sh["flops"] / dur / PEAK_F32, 4))
-            key = "%d,%d,%d" % (sh["M"], sh["N"], sh["K"]) if f.startswith("gemm_") else "tail,%d" % sh["M"]
+            key = ("%d,%d,%d" % (sh["M"], sh["N"], sh["K"]) if f.startswith("gemm_")
+                   else ("tailg,%d" if "gated" in f else "tail,%d") % sh["M"])
             table[key] = ent
             md.append(f"| {sh['M']} | {sh['name']} | {f} | {sh['N']} | {sh['K']} | {ent['dur_us']} | {mops / expect:.3f} | "
                       f"{ent['mfma_tflops']} | {ent['mfma_frac']:.3f} | {ent['busy_per_simd']} | "
