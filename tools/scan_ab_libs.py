@@ -15,12 +15,20 @@ def main():
     libs = sys.argv[3:]
     Di, N, reps = 384, 64, 20
     fns = []
-    for p in libs:
+    for spec in libs:  # path[@key=value]: vasr_set_option(key, value) before each of this entry's launches
+        p, _, opt = spec.partition("@")
         lib = ctypes.CDLL(p)
         f = lib.vasr_ssm_scan_f32
         c_p, c_i64 = ctypes.c_void_p, ctypes.c_int64
         f.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p]
-        fns.append((p.split("/")[-1], f))
+        if opt:
+            key, val = (int(v) for v in opt.split("="))
+            lib.vasr_set_option.argtypes = [ctypes.c_int, ctypes.c_int]
+
+            def f(*a, _f=f, _lib=lib, _k=key, _v=val):
+                assert _lib.vasr_set_option(_k, _v) >= 0
+                return _f(*a)
+        fns.append((spec.split("/")[-1], f))
     data = {}
     for B, L in shapes:
         g = torch.Generator(device="cuda").manual_seed(B * L)
