@@ -209,3 +209,38 @@ def test_chunked_workspace_size():
     assert lib.vasr_ssm_scan_workspace_floats(1, 501, 384, 64) == 4 * 32 * 384 * 64
     assert lib.vasr_ssm_scan_workspace_floats(2, 16, 8, 16) == 4 * 2 * 1 * 8 * 16
     assert lib.vasr_ssm_scan_workspace_floats(0, 16, 8, 16) == 0
+
+
+# ----------------------------------------------------------------------------- ungated form (round 6)
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,Di", [(16, 64), (32, 384), (64, 384), (128, 256)])
+@pytest.mark.parametrize("B,L", [(1, 17), (3, 501), (16, 501), (2, 1501), (1, 4100)])
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("npl,tc", [(4, 16), (2, 16), (4, 32)])
+def test_ungated_scan_is_the_gated_scan_at_unit_gate(N, Di, B, L, mode, npl, tc):
+    """vasr_ssm_scan_ungated_f32 (the z-in-tail block's scan: no z staged, out = y + x D) against the
+    gated streaming kernel with z = 256, where silu(z) is exactly 256 (exp2 underflows to 0, so the
+    reciprocal is of 1): gated = 256 y, a power-of-two scaling, so the two must agree bit for bit --
+    every lane layout, chunk length and upper-stack depth (L up to 4100: levels in LDS)."""
+    import torch
+    from velocity_asr import _lib, ops
+    if N == 128 and npl == 2:
+        pytest.skip("N = 128 runs 4 states per lane only")
+    g = torch.Generator(device="cuda").manual_seed(N * 7 + B * L + mode)
+    M = B * L
+    xz = torch.randn(M, 2 * Di, device="cuda", generator=g)
+    xz[:, Di:] = 256.0
+    dt = torch.nn.functional.softplus(torch.randn(M, Di, device="cuda", generator=g) - 1)
+    bc = torch.randn(M, 2 * N, device="cuda", generator=g)
+    A2 = -(torch.arange(1, N + 1, device="cuda", dtype=torch.float32)
+           + 0.1 * torch.rand(N, device="cuda", generator=g)) * 1.4426950408889634
+    D = 1 + 0.1 * torch.randn(Di, device="cuda", generator=g)
+    prev = ops.scan_form("streaming")
+    try:
+        with ops.option(_lib.OPT_SCAN_LANES, npl), ops.option(_lib.OPT_SCAN_CHUNK, tc):
+            gated = ops.ssm_scan(xz, dt, bc, A2, D, B, L, mode)
+            ungated = ops.ssm_scan_ungated(xz[:, :Di], dt, bc, A2, D, B, L, mode)
+    finally:
+        ops.scan_form(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(gated, ungated * 256.0), (gated - ungated * 256.0).abs().max().item()
