@@ -214,16 +214,21 @@ def isolated_times(model, audio, reps=20):
             from velocity_asr import _lib
             from velocity_asr.ssm import _tree_mode
             Di, N = blk.ssm.d_inner, blk.ssm.state_dim
-            proj = lambda: ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM,  # noqa: E731
-                                    n_out=Di + 2 * N)
-            xbd = proj()
             mode = _tree_mode()
-            out = dict(scan=per_launch(lambda: ops.ssm_scan_ungated(xbd[:, :Di], xbd[:, Di + 2 * N:],
-                                                                    xbd[:, Di:Di + 2 * N], p["A2"], blk.ssm.D, B, L,
-                                                                    mode)),
-                       scan_key=(B, L), gemm=per_launch(proj), gemm_key=(B * L, p["w_noz"].shape[0], D, 1))
-            yd = ops.ssm_scan_ungated(xbd[:, :Di], xbd[:, Di + 2 * N:], xbd[:, Di:Di + 2 * N], p["A2"], blk.ssm.D,
-                                      B, L, mode)
+            if "w_noz" in p:  # fp32: one projection GEMM writes [x | B | C | dt]
+                proj = lambda: ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM,  # noqa: E731
+                                        n_out=Di + 2 * N)
+                xbd = proj()
+                xs, bc, dt = xbd[:, :Di], xbd[:, Di:Di + 2 * N], xbd[:, Di + 2 * N:]
+                out = dict(gemm=per_launch(proj), gemm_key=(B * L, p["w_noz"].shape[0], D, 1))
+            else:  # bf16: in_proj's x rows, then [x_proj; dt_proj]
+                xs = ops.gemm(u, p["w_x"])
+                xdt = ops.gemm(xs, p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=2 * N)
+                bc, dt = xdt[:, :2 * N], xdt[:, 2 * N:]
+                out = {}
+            out.update(scan=per_launch(lambda: ops.ssm_scan_ungated(xs, dt, bc, p["A2"], blk.ssm.D, B, L, mode)),
+                       scan_key=(B, L))
+            yd = ops.ssm_scan_ungated(xs, dt, bc, p["A2"], blk.ssm.D, B, L, mode)
             x2 = x.view(B * L, D)
             out["tail"] = per_launch(lambda: ops.ssm_block_tail_gated(
                 yd, u, p["w_z"], mode, x2, blk.ssm.out_proj.weight, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps,

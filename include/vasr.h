@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 15
+#define VASR_ABI_VERSION 16
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -246,6 +246,16 @@ int vasr_ssm_block_tail_bf16(const float* g, int64_t ldg, const float* x, int64_
                              const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
                              const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
                              int M, int D, int E, void* stream);
+/* The z-in-tail tail for the bf16 model (ABI 16): z = u @ W_z^T with W_z as one
+ * vasr_pack_weights_bf16 plane (the bf16 in_proj rows Di..2Di-1) and u rounded to bf16 at the MFMA
+ * input -- vasr_linear_bf16's exact product --, g = yd * silu(z) rounded to bf16 as the tail
+ * above stages it, then that tail (Wo, W1, W2 as vasr_pack_weights16_bf16 planes).  Bitwise the
+ * output of vasr_ssm_scan_f32 + vasr_ssm_block_tail_bf16 on vasr_linear_bf16's [x | z]. */
+int vasr_ssm_block_tail_gated_bf16(const float* yd, int64_t ldy, const float* u, int64_t ldu, const uint16_t* wz,
+                                   int mode, const float* x, int64_t ldx, const uint16_t* wo16,
+                                   const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                                   const float* b1, const uint16_t* w2_16, const float* b2, float* out, int64_t ldo,
+                                   int M, int D, int E, void* stream);
 int vasr_pack_weights16_bf16(const uint16_t* W, int64_t ldw, int N, int K, uint16_t* out, void* stream);
 int64_t vasr_pack_weights16_bf16_elems(int N, int K);
 /* Split-bf16 planes of a (N, K) fp32 weight in the fragment layout of v_mfma_f32_16x16x32_bf16

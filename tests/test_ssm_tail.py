@@ -168,6 +168,45 @@ def test_z_in_tail_model_logits_bitwise(monkeypatch):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("fma", ["1", "0"], ids=["mode2", "mode0"])
+@pytest.mark.parametrize("B,L", [(9, 501), (11, 1501), (5, 1000)])
+def test_z_in_tail_block_bitwise_bf16(monkeypatch, B, L, fma):
+    """The bf16 model's z-in-tail block (in_proj's x rows alone, ungated scan, tail that forms z
+    with vasr_linear_bf16's one bf16 product per k-step and stages g rounded to bf16) vs the
+    three-launch bf16 block: bitwise equal."""
+    m, _ = _block(2)
+    blk = m.to(torch.bfloat16).local_ssm.layers[2]
+    x = torch.from_numpy(np.random.default_rng(B + L).standard_normal((B, L, 192)).astype(np.float32)).to(DEV)
+    monkeypatch.setenv("VASR_SCAN_FMA", fma)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "1")
+    assert blk._z_in_tail(B, L, 192)
+    a = blk(x)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "0")
+    assert not blk._z_in_tail(B, L, 192)
+    b = blk(x)
+    assert torch.equal(a, b), (a - b).abs().max().item()
+
+
+def test_z_in_tail_model_logits_bitwise_bf16(monkeypatch):
+    """C3's model (bf16 weights) on 32 x 10 s: logits with and without z-in-tail bitwise equal;
+    a mixed-dtype block keeps the gated scan."""
+    import velocity_asr as va
+    from velocity_asr import synthetic as S
+    m, _ = _block(0)
+    m = m.to(torch.bfloat16)
+    blk = m.local_ssm.layers[0]
+    assert blk._z_in_tail(32, 501, 192)
+    mel = va.compute_mel_spectrogram(torch.from_numpy(S.make_audio(32, 160000, seed=4321)).to(DEV))
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "1")
+    a = m(mel)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "0")
+    b = m(mel)
+    assert torch.equal(a, b)
+    monkeypatch.setenv("VASR_Z_IN_TAIL", "1")
+    blk.ffn[0].float()
+    assert not blk._z_in_tail(32, 501, 192)
+
+
 def test_z_in_tail_argument_checks():
     from velocity_asr import _lib
     lib = _lib.lib()
@@ -178,3 +217,8 @@ def test_z_in_tail_argument_checks():
     assert lib.vasr_ssm_block_tail_gated_f32(p, 384, None, 192, p, 2, p, 192, p, p, p, 1e-5, p, p, p, p, p, 192,
                                              1, 192, 384, None) == -1
     assert b"u" in lib.vasr_last_error()
+    assert lib.vasr_ssm_block_tail_gated_bf16(p, 384, p, 192, None, 2, p, 192, p, p, p, 1e-5, p, p, p, p, p, 192,
+                                              1, 192, 384, None) == -1
+    assert lib.vasr_ssm_block_tail_gated_bf16(p, 384, p, 192, p, 1, p, 192, p, p, p, 1e-5, p, p, p, p, p, 192,
+                                              1, 192, 384, None) == -1
+    assert b"mode" in lib.vasr_last_error()

@@ -338,31 +338,39 @@ struct GateParams {
     const uint16_t* wz;   // W_z = in_proj rows Di..2Di-1 as vasr_split_weights_bf16x3 planes
 };
 
-// g = y * silu(z) split into R's three planes, with contraction off for the product AND the split:
-// left to the default (fp-contract=fast) the compiler forms the split's residual g - hi as one fma
-// from the unrounded product, i.e. planes of a more exact g than the scan writes (1e-6 differences
-// at the block output; the scan TU is built with -ffp-contract=off).  z + 0.0f: the projection's
-// epilogue adds its zero bias to the z columns (the same sign of a zero).
-template <int MODE>
+// g = y * silu(z) into R's NP planes, with contraction off for the product AND the split: left to the
+// default (fp-contract=fast) the compiler forms the split's residual g - hi as one fma from the
+// unrounded product, i.e. planes of a more exact g than the scan writes (1e-6 differences at the block
+// output; the scan TU is built with -ffp-contract=off).  NP = 3 (fp32 model): z + 0.0f, as the
+// projection's epilogue adds its zero bias to the z columns (the same sign of a zero); NP = 1 (bf16
+// model): in_proj has no bias and the one plane is g rounded to bf16, as the bf16 tail's staging does.
+template <int MODE, int NP>
 __device__ __forceinline__ void gate_split_store(char* plane0, int plane_bytes, int off, float y, float z) {
 #pragma clang fp contract(off)
-    const float v = y * silu_of<MODE>(z + 0.0f);
-    const __bf16 hi = (__bf16)v;
-    const float r1 = v - (float)hi;
-    const __bf16 mid = (__bf16)r1;
-    const __bf16 lo = (__bf16)(r1 - (float)mid);
-    *reinterpret_cast<__bf16*>(plane0 + off) = hi;
-    *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = mid;
-    *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = lo;
+    if constexpr (NP == 3) {
+        const float v = y * silu_of<MODE>(z + 0.0f);
+        const __bf16 hi = (__bf16)v;
+        const float r1 = v - (float)hi;
+        const __bf16 mid = (__bf16)r1;
+        const __bf16 lo = (__bf16)(r1 - (float)mid);
+        *reinterpret_cast<__bf16*>(plane0 + off) = hi;
+        *reinterpret_cast<__bf16*>(plane0 + plane_bytes + off) = mid;
+        *reinterpret_cast<__bf16*>(plane0 + 2 * plane_bytes + off) = lo;
+    } else {
+        *reinterpret_cast<__bf16*>(plane0 + off) = (__bf16)(y * silu_of<MODE>(z));
+    }
 }
 
-template <int MODE>
+// NP = 3: the fp32 model (split planes; z by the rows / tile engines' six products per k-step).
+// NP = 1: the bf16 model (one bf16 plane; z by the bf16 tile engine's one product per k-step, A = u
+// rounded to bf16, W_z as vasr_pack_weights_bf16's layout).
+template <int MODE, int NP>
 __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, GateParams G) {
-    using Ctx = TailCtx<3, 2, 1>;
+    using Ctx = TailCtx<NP, 2, 1>;
     constexpr int NT = 768;
     constexpr int KSZ = TD / 16;  // z k-steps (16 k each)
-    __shared__ __attribute__((aligned(16))) char R[3 * Ctx::PE];
-    __shared__ __attribute__((aligned(16))) char H[3 * Ctx::PDB];
+    __shared__ __attribute__((aligned(16))) char R[NP * Ctx::PE];
+    __shared__ __attribute__((aligned(16))) char H[NP * Ctx::PDB];
     Ctx c{P, R, H};
     c.lane = threadIdx.x & 63;
     c.wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -371,13 +379,13 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
     c.m0 = blockIdx.x * Ctx::ROWS;
     const int zr = c.lane & 31, zh = c.lane >> 5;  // 32x32x16 operand map: row / column zr, k half zh
     const int zcol = 32 * c.wave + zr;
-    // W_z fragments of k-steps 0 and 1 (chunk `wave` of the split layout: [KSZ][3][64 lanes][16 B])
-    const char* wzc = reinterpret_cast<const char*>(G.wz) + (int64_t)c.wave * KSZ * 3 * 1024 + c.lane * 16;
-    bf16x8 wf[3][3];
+    // W_z fragments of k-steps 0 and 1 (chunk `wave` of the layout: [KSZ][NP][64 lanes][16 B])
+    const char* wzc = reinterpret_cast<const char*>(G.wz) + (int64_t)c.wave * KSZ * NP * 1024 + c.lane * 16;
+    bf16x8 wf[3][NP];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) wf[ks][pl] = *reinterpret_cast<const bf16x8*>(wzc + (ks * 3 + pl) * 1024);
+        for (int pl = 0; pl < NP; ++pl) wf[ks][pl] = *reinterpret_cast<const bf16x8*>(wzc + (ks * NP + pl) * 1024);
     // y + x D at this lane's z positions (rows (i & 3) + 8 (i >> 2) + 4 zh of the tile)
     float yv[16];
 #pragma unroll
@@ -385,22 +393,22 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
         const int row = c.m0 + (i & 3) + 8 * (i >> 2) + 4 * zh;
         yv[i] = row < P.M ? G.yd[(int64_t)row * G.ldy + zcol] : 0.0f;
     }
-    // u tile -> H's three planes (192-wide layout; rows past M repeat row M - 1, never stored)
+    // u tile -> H's NP planes (192-wide layout; rows past M repeat row M - 1, never stored)
     {
         static_assert(Ctx::ROWS * TD / 8 == NT, "one 8-float chunk of u per thread");
         const int rr = threadIdx.x / (TD / 8), ch = threadIdx.x - rr * (TD / 8);
         const float* src = G.u + (int64_t)min(c.m0 + rr, P.M - 1) * G.ldu + 8 * ch;
         const float4 v0 = *reinterpret_cast<const float4*>(src);
         const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
-        split_store8<3>(H, Ctx::PDB, rr * TD * 2 + ((ch ^ (rr & 7)) << 4), v0, v1);
+        split_store8<NP>(H, Ctx::PDB, rr * TD * 2 + ((ch ^ (rr & 7)) << 4), v0, v1);
     }
     lds_barrier();  // u planes complete
-    auto read_u = [&](int ks, bf16x8 (&a)[3]) {
+    auto read_u = [&](int ks, bf16x8 (&a)[NP]) {
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < NP; ++pl)
             a[pl] = *reinterpret_cast<const bf16x8*>(H + pl * Ctx::PDB + zr * TD * 2 + (((2 * ks + zh) ^ (zr & 7)) << 4));
     };
-    bf16x8 af[2][3];
+    bf16x8 af[2][NP];
     read_u(0, af[0]);
     floatx16 zc;
 #pragma unroll
@@ -409,29 +417,31 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
     for (int ks = 0; ks < KSZ; ++ks) {
         if (ks + 2 < KSZ) {
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-                wf[(ks + 2) % 3][pl] = *reinterpret_cast<const bf16x8*>(wzc + ((ks + 2) * 3 + pl) * 1024);
+            for (int pl = 0; pl < NP; ++pl)
+                wf[(ks + 2) % 3][pl] = *reinterpret_cast<const bf16x8*>(wzc + ((ks + 2) * NP + pl) * 1024);
         }
         if (ks + 1 < KSZ) read_u(ks + 1, af[(ks + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
-        const bf16x8(&a)[3] = af[ks & 1];
-        const bf16x8(&w)[3] = wf[ks % 3];
-        // gemm_rows.hip's order: small terms first, then the leading hi * hi term
-        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], w[0], zc, 0, 0, 0);
-        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[2], zc, 0, 0, 0);
-        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[1], zc, 0, 0, 0);
-        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[0], zc, 0, 0, 0);
-        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[1], zc, 0, 0, 0);
+        const bf16x8(&a)[NP] = af[ks & 1];
+        const bf16x8(&w)[NP] = wf[ks % 3];
+        if constexpr (NP == 3) {
+            // gemm_rows.hip's order: small terms first, then the leading hi * hi term
+            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], w[0], zc, 0, 0, 0);
+            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[2], zc, 0, 0, 0);
+            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[1], zc, 0, 0, 0);
+            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[0], zc, 0, 0, 0);
+            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[1], zc, 0, 0, 0);
+        }
         zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[0], zc, 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
     // the first PD steps' weights of the tail's own stream, in flight during the gate
-    load_first<0, 3, 2, 1>(c);
+    load_first<0, NP, 2, 1>(c);
     // g = (y + x D) * silu(z) into R's planes
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int rl = (i & 3) + 8 * (i >> 2) + 4 * zh;
-        gate_split_store<MODE>(R, Ctx::PE, poff<TE>(rl, zcol), yv[i], zc[i]);
+        gate_split_store<MODE, NP>(R, Ctx::PE, poff<TE>(rl, zcol), yv[i], zc[i]);
     }
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
@@ -452,7 +462,7 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
         c.lnb[i] = P.ln_b[c.lane + 64 * i];
     }
     lds_barrier();  // the g planes are complete (and every wave is past its u reads: H is free for h)
-    tail_step<0, 3, 2, 1>(c);
+    tail_step<0, NP, 2, 1>(c);
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
         const int col = 16 * c.wave + c.r;
@@ -642,7 +652,29 @@ VASR_API int vasr_ssm_block_tail_gated_f32(const float* yd, int64_t ldy, const f
     const TailParams p{yd, ldy, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
     const GateParams gp{yd, ldy, u, ldu, wz};
     const dim3 grid((unsigned)((M + 31) / 32)), block(768);
-    if (mode == 2) hipLaunchKernelGGL(ssm_tail_gated_kernel<2>, grid, block, 0, as_stream(stream), p, gp);
-    else hipLaunchKernelGGL(ssm_tail_gated_kernel<0>, grid, block, 0, as_stream(stream), p, gp);
+    if (mode == 2) hipLaunchKernelGGL((ssm_tail_gated_kernel<2, 3>), grid, block, 0, as_stream(stream), p, gp);
+    else hipLaunchKernelGGL((ssm_tail_gated_kernel<0, 3>), grid, block, 0, as_stream(stream), p, gp);
     return launch_status("vasr_ssm_block_tail_gated_f32");
+}
+
+VASR_API int vasr_ssm_block_tail_gated_bf16(const float* yd, int64_t ldy, const float* u, int64_t ldu, const uint16_t* wz,
+                                            int mode, const float* x, int64_t ldx, const uint16_t* wo16,
+                                            const float* ln_w, const float* ln_b, float ln_eps, const uint16_t* w1_16,
+                                            const float* b1, const uint16_t* w2_16, const float* b2, float* out,
+                                            int64_t ldo, int M, int D, int E, void* stream) {
+    using namespace vasr;
+    if (int rc = tail_args(yd, ldy, x, ldx, wo16, ln_w, ln_b, w1_16, b1, w2_16, b2, out, ldo, M, D, E,
+                           "vasr_ssm_block_tail_gated_bf16"))
+        return rc;
+    VASR_CHECK_ARG(u && wz && ldu >= D && ldu % 4 == 0 && (reinterpret_cast<uintptr_t>(u) & 15) == 0 &&
+                       (reinterpret_cast<uintptr_t>(wz) & 15) == 0,
+                   "vasr_ssm_block_tail_gated_bf16: u (16-B aligned rows, ldu >= D, ldu %% 4 == 0) and wz needed");
+    VASR_CHECK_ARG(mode == 0 || mode == 2, "vasr_ssm_block_tail_gated_bf16: mode must be 0 or 2 (the scan's gate)");
+    if (M == 0) return VASR_OK;
+    const TailParams p{yd, ldy, x, ldx, wo16, ln_w, ln_b, ln_eps, w1_16, b1, w2_16, b2, out, ldo, M};
+    const GateParams gp{yd, ldy, u, ldu, wz};
+    const dim3 grid((unsigned)((M + 31) / 32)), block(768);
+    if (mode == 2) hipLaunchKernelGGL((ssm_tail_gated_kernel<2, 1>), grid, block, 0, as_stream(stream), p, gp);
+    else hipLaunchKernelGGL((ssm_tail_gated_kernel<0, 1>), grid, block, 0, as_stream(stream), p, gp);
+    return launch_status("vasr_ssm_block_tail_gated_bf16");
 }

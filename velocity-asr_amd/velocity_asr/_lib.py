@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -71,6 +71,8 @@ _SIGNATURES = {
                                 + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_ssm_block_tail_gated_f32": ([c_p, c_i64, c_p, c_i64, c_p, ctypes.c_int, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p,
                                        c_p, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
+    "vasr_ssm_block_tail_gated_bf16": ([c_p, c_i64, c_p, c_i64, c_p, ctypes.c_int, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p,
+                                        c_p, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_ssm_block_tail_bf16": ([c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_i64]
                                  + [ctypes.c_int] * 3 + [c_p], ctypes.c_int),
     "vasr_pack_weights16_bf16": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),

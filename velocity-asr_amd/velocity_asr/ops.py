@@ -562,12 +562,19 @@ def ssm_block_tail_gated(yd: torch.Tensor, u: torch.Tensor, wz: torch.Tensor, mo
                          wo: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, ln_eps: float, w1: torch.Tensor,
                          b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """The z-in-tail block's tail (vasr_ssm_block_tail_gated_f32): z = u W_z^T (the split GEMM's
-    exact product), g = yd * silu(z) (scan mode `mode`'s gate), then ssm_block_tail on g -- for
-    yd (M, 384) the ungated scan output, u (M, 192) the projection input, wz (384, 192) = in_proj
-    rows Di..2Di-1 (a persistent tensor: its split planes are cached by identity)."""
-    for n, t in (("yd", yd), ("u", u), ("wz", wz), ("x", x), ("ln_w", ln_w), ("ln_b", ln_b), ("b1", b1), ("b2", b2),
-                 ("wo", wo), ("w1", w1), ("w2", w2)):
+    """The z-in-tail block's tail (vasr_ssm_block_tail_gated_f32, or _bf16 for bf16 weights): z =
+    u W_z^T (the projection GEMM's exact product: split planes for fp32 weights, the bf16 tile
+    engine's one product for bf16), g = yd * silu(z) (scan mode `mode`'s gate), then
+    ssm_block_tail on g -- for yd (M, 384) the ungated scan output, u (M, 192) the projection
+    input, wz (384, 192) = in_proj rows Di..2Di-1 (a persistent tensor: its planes are cached by
+    identity)."""
+    bf16 = wo.dtype == torch.bfloat16
+    if bf16:
+        if not (wz.dtype == w1.dtype == w2.dtype == torch.bfloat16):
+            raise TypeError("ssm_block_tail_gated: mixed weight dtypes")
+        ln_w, ln_b, b1, b2 = f32(ln_w), f32(ln_b), f32(b1), f32(b2)
+    for n, t in (("yd", yd), ("u", u), ("x", x), ("ln_w", ln_w), ("ln_b", ln_b), ("b1", b1), ("b2", b2)) + (
+            () if bf16 else (("wz", wz), ("wo", wo), ("w1", w1), ("w2", w2))):
         _cuda_f32(f"ssm_block_tail_gated.{n}", t)
     M, E, ldy = _rows("ssm_block_tail_gated.yd", yd)
     Mu, D, ldu = _rows("ssm_block_tail_gated.u", u)
@@ -577,14 +584,13 @@ def ssm_block_tail_gated(yd: torch.Tensor, u: torch.Tensor, wz: torch.Tensor, mo
     if out is None:
         out = torch.empty((M, D), device=yd.device, dtype=torch.float32)
     _, _, ldo = _rows("ssm_block_tail_gated.out", out)
+    zprep, prep = (pack_bf16, pack_weights16) if bf16 else (split_weights, split_weights16)
+    fn = "vasr_ssm_block_tail_gated_bf16" if bf16 else "vasr_ssm_block_tail_gated_f32"
     ev = _t0("ssm_tail")
-    check(L.lib().vasr_ssm_block_tail_gated_f32(yd.data_ptr(), ldy, u.data_ptr(), ldu, split_weights(wz).data_ptr(),
-                                                int(mode), x.data_ptr(), ldx, split_weights16(wo).data_ptr(),
-                                                ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(),
-                                                float(ln_eps), split_weights16(w1).data_ptr(),
-                                                b1.contiguous().data_ptr(), split_weights16(w2).data_ptr(),
-                                                b2.contiguous().data_ptr(), out.data_ptr(), ldo, M, D, E,
-                                                stream_of(yd)), "vasr_ssm_block_tail_gated_f32")
+    check(getattr(L.lib(), fn)(yd.data_ptr(), ldy, u.data_ptr(), ldu, zprep(wz).data_ptr(), int(mode), x.data_ptr(),
+                               ldx, prep(wo).data_ptr(), ln_w.contiguous().data_ptr(), ln_b.contiguous().data_ptr(),
+                               float(ln_eps), prep(w1).data_ptr(), b1.contiguous().data_ptr(), prep(w2).data_ptr(),
+                               b2.contiguous().data_ptr(), out.data_ptr(), ldo, M, D, E, stream_of(yd)), fn)
     _t1("ssm_tail", ev, dict(M=M, D=D, E=E, gated=True))
     return out
 

@@ -104,6 +104,13 @@ class SelectiveSSM(nn.Module):
                 out["w_noz"] = torch.cat([self.in_proj.weight.detach()[:Di], wc], 0).contiguous()
                 out["b_noz"] = torch.cat([torch.zeros(Di, device=dev), b]).contiguous()
                 out["w_z"] = self.in_proj.weight.detach()[Di:].contiguous()
+            elif w.dtype == torch.bfloat16 and self.in_proj.weight.dtype == torch.bfloat16:
+                # the bf16 model's z-in-tail block: in_proj split into its x rows (the projection
+                # GEMM) and its z rows (the tail's product); the bf16 engine's per-column result
+                # does not depend on the other columns, so both are bitwise in_proj's
+                Di = self.d_inner
+                out["w_x"] = self.in_proj.weight.detach()[:Di].contiguous()
+                out["w_z"] = self.in_proj.weight.detach()[Di:].contiguous()
             return out
         return cached(self, "ssm", (self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, self.A_log,
                                     self.in_proj.weight), build)
@@ -190,29 +197,35 @@ class SSMBlock(nn.Module):
         return self.tail(g, x2, B, L)
 
     # z-in-tail: z = in_proj_z(u) feeds only the gate y * silu(z)
-    # (ssm.py:106, :129).  The projection GEMM -- bound by its C stores -- then writes
-    # [x | B | C | dt] (896 of its 1280 columns), the scan writes the ungated y + x D, and the fused
-    # tail forms z itself with the split GEMM's exact product before applying the gate and the
-    # usual tail: bitwise the three-launch block's output (tests/test_ssm_tail.py).  Where it runs:
-    # the fp32 model with the composed projection, the tree scan streamed (ops._use_chunked false)
-    # and the 32-row tail (M > 4096 token rows: the bench's batches); VASR_Z_IN_TAIL=0 turns it off.
+    # (ssm.py:106, :129).  The projection GEMM -- bound by its C stores -- then
+    # skips the z columns, the scan writes the ungated y + x D, and the fused tail forms z itself
+    # with the projection GEMM's exact product before applying the gate and the usual tail:
+    # bitwise the three-launch block's output (tests/test_ssm_tail.py).  fp32 model: the composed
+    # projection writes [x | B | C | dt] (896 of its 1280 columns).  bf16 model: in_proj writes x
+    # alone (384 of 768 columns), [x_proj; dt_proj] reads it as before.  Where it runs: the tree
+    # scan streamed (ops._use_chunked false) and the 32-row tail (M > 4096 token rows: the
+    # bench's batches); VASR_Z_IN_TAIL=0 turns it off.
     Z_IN_TAIL_MIN_ROWS = 4097
 
     def _z_in_tail(self, B: int, L: int, D: int) -> bool:
         ssm = self.ssm
         if os.environ.get("VASR_Z_IN_TAIL", "1") == "0" or B * L < self.Z_IN_TAIL_MIN_ROWS:
             return False
-        if _SCAN_MODE_ID[ssm.scan_mode] != 0 or os.environ.get("VASR_XDT_COMPOSE", "1") == "0":
+        if _SCAN_MODE_ID[ssm.scan_mode] != 0:
             return False
         mods = (ssm.in_proj, ssm.x_proj, ssm.dt_proj, ssm.out_proj, self.ffn[0], self.ffn[3])
-        if not all(type(m) is nn.Linear and m.weight.dtype == torch.float32 for m in mods):
-            return False  # QAT (quantize.QuantizedLinear) and bf16 models keep the gated scan
+        dtype = ssm.in_proj.weight.dtype
+        if dtype not in (torch.float32, torch.bfloat16) or not all(
+                type(m) is nn.Linear and m.weight.dtype == dtype for m in mods):
+            return False  # QAT (quantize.QuantizedLinear) and mixed-dtype models keep the gated scan
+        if dtype == torch.float32 and os.environ.get("VASR_XDT_COMPOSE", "1") == "0":
+            return False
         if not self._fused_tail_ok(D):
             return False
         N = ops.scan_state_dim(ssm.state_dim)
         if N != ssm.state_dim or ops._use_chunked(B, L, ssm.d_inner, N, _tree_mode()):
             return False
-        return "w_noz" in ssm._prepared()
+        return ("w_noz" if dtype == torch.float32 else "w_x") in ssm._prepared()
 
     def _forward_z_in_tail(self, x: torch.Tensor) -> torch.Tensor:
         B, L, D = x.shape
@@ -223,9 +236,15 @@ class SSMBlock(nn.Module):
         x2 = x.view(B * L, D)
         u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
                           self.conv.bias, self.norm1.eps).view(B * L, D)
-        xbd = ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=Di + 2 * N)  # [x | B | C | dt]
+        if "w_noz" in p:
+            xbd = ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=Di + 2 * N)  # [x|B|C|dt]
+            xs, bc, dt = xbd[:, :Di], xbd[:, Di:Di + 2 * N], xbd[:, Di + 2 * N:]
+        else:
+            xs = ops.gemm(u, p["w_x"])                                                 # (M, Di) x
+            xdt = ops.gemm(xs, p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=2 * N)  # [B|C|dt]
+            bc, dt = xdt[:, :2 * N], xdt[:, 2 * N:]
         mode = _tree_mode()
-        yd = ops.ssm_scan_ungated(xbd[:, :Di], xbd[:, Di + 2 * N:], xbd[:, Di:Di + 2 * N], p["A2"], ssm.D, B, L, mode)
+        yd = ops.ssm_scan_ungated(xs, dt, bc, p["A2"], ssm.D, B, L, mode)
         out = ops.ssm_block_tail_gated(yd, u, p["w_z"], mode, x2, ssm.out_proj.weight, self.norm2.weight,
                                        self.norm2.bias, self.norm2.eps, self.ffn[0].weight, self.ffn[0].bias,
                                        self.ffn[3].weight, self.ffn[3].bias)
