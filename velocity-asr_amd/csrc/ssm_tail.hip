@@ -110,7 +110,19 @@ struct TailCtx {
     bf16x8 w[RING][CT][NP];  // [ring slot][column tile][plane]
     float x1[RT][CT][4];     // residual x, then x1 = out_proj(g) + x
     float bb1[2][CT], bb2[CT], lnw[3], lnb[3];
+#ifdef VASR_TAIL_STAMPS
+    uint64_t ts[10];  // diagnostic builds: s_memtime at the phase boundaries (wave 0)
+#endif
 };
+
+#ifdef VASR_TAIL_STAMPS
+// Diagnostic builds only (-DVASR_TAIL_STAMPS, tools/diag/tail_stamps.py): per workgroup of the gated
+// tail, 12 int64: HW_ID | XCC << 32, s_memrealtime at entry and exit, s_memtime at 9 phase boundaries.
+__device__ int64_t* g_tail_stamps;
+#define TAIL_STAMP(c, i) ((c).ts[i] = __builtin_amdgcn_s_memtime())
+#else
+#define TAIL_STAMP(c, i) ((void)0)
+#endif
 
 // weight fragments of step S for this wave: column tiles CT w .. CT w + CT - 1, NP planes, from the
 // fragment layout [N/16][K/32][NP][64][8]
@@ -234,6 +246,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
                 split_store<NP>(c.H, Ctx::PDB, poff<TD>(rr, c.lane + 64 * i), __builtin_fmaf((v[i] - mean) * rstd, c.lnw[i], c.lnb[i]));
         }
         lds_barrier();  // h complete; the scratch in R is free for f
+        TAIL_STAMP(c, 5);
     } else if constexpr (S == 17 || S == 23) {
         // f = GELU(ffn.0(h) + b1), FFN1 column half hh, split into the planes of R
         constexpr int hh = S == 17 ? 0 : 1;
@@ -248,7 +261,10 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
                                 gelu_fast(c.acc[tm][t][i] + c.bb1[hh][t]));
                 c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
-        if constexpr (S == 23) lds_barrier();  // f complete before FFN2 reads it
+        if constexpr (S == 23) {
+            lds_barrier();  // f complete before FFN2 reads it
+            TAIL_STAMP(c, 6);
+        }
     }
     if constexpr (S + 1 < NSTAGES) tail_step<S + 1, NP, RT, CT>(c);
 }
@@ -361,9 +377,46 @@ __device__ __forceinline__ void gate_split_store(char* plane0, int plane_bytes, 
     }
 }
 
+// four consecutive columns of one row (one 8-B piece per plane): the same float operations per value
+template <int MODE, int NP>
+__device__ __forceinline__ void gate_split_store4(char* plane0, int plane_bytes, int off, const float4& y,
+                                                  const floatx4& z) {
+#pragma clang fp contract(off)
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const float yy[4] = {y.x, y.y, y.z, y.w};
+    bf16x4 hi, mid, lo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (NP == 3) {
+            const float v = yy[i] * silu_of<MODE>(z[i] + 0.0f);
+            hi[i] = (__bf16)v;
+            const float r1 = v - (float)hi[i];
+            mid[i] = (__bf16)r1;
+            lo[i] = (__bf16)(r1 - (float)mid[i]);
+        } else {
+            hi[i] = (__bf16)(yy[i] * silu_of<MODE>(z[i]));
+        }
+    }
+    *reinterpret_cast<bf16x4*>(plane0 + off) = hi;
+    if constexpr (NP == 3) {
+        *reinterpret_cast<bf16x4*>(plane0 + plane_bytes + off) = mid;
+        *reinterpret_cast<bf16x4*>(plane0 + 2 * plane_bytes + off) = lo;
+    }
+}
+
 // NP = 3: the fp32 model (split planes; z by the rows / tile engines' six products per k-step).
 // NP = 1: the bf16 model (one bf16 plane; z by the bf16 tile engine's one product per k-step, A = u
 // rounded to bf16, W_z as vasr_pack_weights_bf16's layout).
+#ifndef VASR_TAILG_ZPD
+#define VASR_TAILG_ZPD 2
+#endif
+// SWAP: z^T = W_z u^T (the same MFMAs with the operands exchanged: each output element is the same dot
+// product of the same bf16 pairs in the same k order), so a lane holds 16 z columns of ONE token in
+// four runs of four: y + x D arrives as four float4 loads and g leaves as one 8-B store per run and
+// plane (instead of 16 scalar loads and 16 x NP two-byte stores); the u tile's loads go first
+#ifndef VASR_TAILG_SWAP
+#define VASR_TAILG_SWAP 1
+#endif
 template <int MODE, int NP>
 __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, GateParams G) {
     using Ctx = TailCtx<NP, 2, 1>;
@@ -377,15 +430,42 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
     c.r = c.lane & 15;
     c.q = c.lane >> 4;
     c.m0 = blockIdx.x * Ctx::ROWS;
+#ifdef VASR_TAIL_STAMPS
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    TAIL_STAMP(c, 0);
     const int zr = c.lane & 31, zh = c.lane >> 5;  // 32x32x16 operand map: row / column zr, k half zh
     const int zcol = 32 * c.wave + zr;
-    // W_z fragments of k-steps 0 and 1 (chunk `wave` of the layout: [KSZ][NP][64 lanes][16 B])
+    // W_z fragments of k-steps 0 .. ZPD-1 (chunk `wave` of the layout: [KSZ][NP][64 lanes][16 B])
+    constexpr int ZPD = VASR_TAILG_ZPD;  // k-steps of W_z in flight
     const char* wzc = reinterpret_cast<const char*>(G.wz) + (int64_t)c.wave * KSZ * NP * 1024 + c.lane * 16;
-    bf16x8 wf[3][NP];
+    bf16x8 wf[ZPD + 1][NP];
+    static_assert(Ctx::ROWS * TD / 8 == NT, "one 8-float chunk of u per thread");
+    const int urr = threadIdx.x / (TD / 8), uch = threadIdx.x - urr * (TD / 8);
+    float4 uv0, uv1;
+#if VASR_TAILG_SWAP
+    // the u tile's loads first: its LDS image is the first thing every wave waits for
+    {
+        const float* src = G.u + (int64_t)min(c.m0 + urr, P.M - 1) * G.ldu + 8 * uch;
+        uv0 = *reinterpret_cast<const float4*>(src);
+        uv1 = *reinterpret_cast<const float4*>(src + 4);
+    }
+#endif
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < ZPD; ++ks)
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl) wf[ks][pl] = *reinterpret_cast<const bf16x8*>(wzc + (ks * NP + pl) * 1024);
+#if VASR_TAILG_SWAP
+    // y + x D of token zr at z columns 32 w + 8 j + 4 zh .. + 3 (j = 0..3)
+    float4 yv4[4];
+    {
+        const int row = c.m0 + zr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            yv4[j] = row < P.M ? *reinterpret_cast<const float4*>(G.yd + (int64_t)row * G.ldy + 32 * c.wave + 8 * j + 4 * zh)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#else
     // y + x D at this lane's z positions (rows (i & 3) + 8 (i >> 2) + 4 zh of the tile)
     float yv[16];
 #pragma unroll
@@ -393,16 +473,16 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
         const int row = c.m0 + (i & 3) + 8 * (i >> 2) + 4 * zh;
         yv[i] = row < P.M ? G.yd[(int64_t)row * G.ldy + zcol] : 0.0f;
     }
-    // u tile -> H's NP planes (192-wide layout; rows past M repeat row M - 1, never stored)
     {
-        static_assert(Ctx::ROWS * TD / 8 == NT, "one 8-float chunk of u per thread");
-        const int rr = threadIdx.x / (TD / 8), ch = threadIdx.x - rr * (TD / 8);
-        const float* src = G.u + (int64_t)min(c.m0 + rr, P.M - 1) * G.ldu + 8 * ch;
-        const float4 v0 = *reinterpret_cast<const float4*>(src);
-        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
-        split_store8<NP>(H, Ctx::PDB, rr * TD * 2 + ((ch ^ (rr & 7)) << 4), v0, v1);
+        const float* src = G.u + (int64_t)min(c.m0 + urr, P.M - 1) * G.ldu + 8 * uch;
+        uv0 = *reinterpret_cast<const float4*>(src);
+        uv1 = *reinterpret_cast<const float4*>(src + 4);
     }
+#endif
+    // u tile -> H's NP planes (192-wide layout; rows past M repeat row M - 1, never stored)
+    split_store8<NP>(H, Ctx::PDB, urr * TD * 2 + ((uch ^ (urr & 7)) << 4), uv0, uv1);
     lds_barrier();  // u planes complete
+    TAIL_STAMP(c, 1);
     auto read_u = [&](int ks, bf16x8 (&a)[NP]) {
 #pragma unroll
         for (int pl = 0; pl < NP; ++pl)
@@ -415,34 +495,48 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
     for (int i = 0; i < 16; ++i) zc[i] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KSZ; ++ks) {
-        if (ks + 2 < KSZ) {
+        if (ks + ZPD < KSZ) {
 #pragma unroll
             for (int pl = 0; pl < NP; ++pl)
-                wf[(ks + 2) % 3][pl] = *reinterpret_cast<const bf16x8*>(wzc + ((ks + 2) * NP + pl) * 1024);
+                wf[(ks + ZPD) % (ZPD + 1)][pl] = *reinterpret_cast<const bf16x8*>(wzc + ((ks + ZPD) * NP + pl) * 1024);
         }
         if (ks + 1 < KSZ) read_u(ks + 1, af[(ks + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8(&a)[NP] = af[ks & 1];
-        const bf16x8(&w)[NP] = wf[ks % 3];
+        const bf16x8(&w)[NP] = wf[ks % (ZPD + 1)];
+#if VASR_TAILG_SWAP
+#define ZMFMA(x, y) __builtin_amdgcn_mfma_f32_32x32x16_bf16(y, x, zc, 0, 0, 0)
+#else
+#define ZMFMA(x, y) __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, zc, 0, 0, 0)
+#endif
         if constexpr (NP == 3) {
             // gemm_rows.hip's order: small terms first, then the leading hi * hi term
-            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], w[0], zc, 0, 0, 0);
-            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[2], zc, 0, 0, 0);
-            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[1], zc, 0, 0, 0);
-            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], w[0], zc, 0, 0, 0);
-            zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[1], zc, 0, 0, 0);
+            zc = ZMFMA(a[2], w[0]);
+            zc = ZMFMA(a[0], w[2]);
+            zc = ZMFMA(a[1], w[1]);
+            zc = ZMFMA(a[1], w[0]);
+            zc = ZMFMA(a[0], w[1]);
         }
-        zc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], w[0], zc, 0, 0, 0);
+        zc = ZMFMA(a[0], w[0]);
+#undef ZMFMA
         __builtin_amdgcn_sched_barrier(0);
     }
     // the first PD steps' weights of the tail's own stream, in flight during the gate
+    TAIL_STAMP(c, 2);
     load_first<0, NP, 2, 1>(c);
     // g = (y + x D) * silu(z) into R's planes
+#if VASR_TAILG_SWAP
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        gate_split_store4<MODE, NP>(R, Ctx::PE, poff<TE>(zr, 32 * c.wave + 8 * j + 4 * zh), yv4[j],
+                                    floatx4{zc[4 * j], zc[4 * j + 1], zc[4 * j + 2], zc[4 * j + 3]});
+#else
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int rl = (i & 3) + 8 * (i >> 2) + 4 * zh;
         gate_split_store<MODE, NP>(R, Ctx::PE, poff<TE>(rl, zcol), yv[i], zc[i]);
     }
+#endif
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
         const int col = 16 * c.wave + c.r;
@@ -461,8 +555,11 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
         c.lnw[i] = P.ln_w[c.lane + 64 * i];
         c.lnb[i] = P.ln_b[c.lane + 64 * i];
     }
+    TAIL_STAMP(c, 3);
     lds_barrier();  // the g planes are complete (and every wave is past its u reads: H is free for h)
+    TAIL_STAMP(c, 4);
     tail_step<0, NP, 2, 1>(c);
+    TAIL_STAMP(c, 7);
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm) {
         const int col = 16 * c.wave + c.r;
@@ -472,6 +569,21 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
             if (row < P.M) P.out[(int64_t)row * P.ldo + col] = (c.acc[tm][0][i] + c.bb2[0]) + c.x1[tm][0][i];
         }
     }
+#ifdef VASR_TAIL_STAMPS
+    TAIL_STAMP(c, 8);
+    if (threadIdx.x == 0 && g_tail_stamps) {
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        uint32_t xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        int64_t* o = g_tail_stamps + 12 * (int64_t)blockIdx.x;
+        o[0] = (int64_t)hw | ((int64_t)(xcc & 0xF) << 32);
+        o[1] = (int64_t)rt0;
+        o[2] = (int64_t)rt1;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) o[3 + i] = (int64_t)c.ts[i];
+    }
+#endif
 }
 
 // Fragment layout of v_mfma_f32_16x16x32_bf16's B operand, three split planes:
@@ -656,6 +768,12 @@ VASR_API int vasr_ssm_block_tail_gated_f32(const float* yd, int64_t ldy, const f
     else hipLaunchKernelGGL((ssm_tail_gated_kernel<0, 3>), grid, block, 0, as_stream(stream), p, gp);
     return launch_status("vasr_ssm_block_tail_gated_f32");
 }
+
+#ifdef VASR_TAIL_STAMPS
+VASR_API int vasr_diag_tail_stamps(void* buf) {  // diagnostic builds only
+    return hipMemcpyToSymbol(HIP_SYMBOL(vasr::g_tail_stamps), &buf, sizeof(buf)) == hipSuccess ? VASR_OK : VASR_EINVAL;
+}
+#endif
 
 VASR_API int vasr_ssm_block_tail_gated_bf16(const float* yd, int64_t ldy, const float* u, int64_t ldu, const uint16_t* wz,
                                             int mode, const float* x, int64_t ldx, const uint16_t* wo16,
