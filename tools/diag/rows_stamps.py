@@ -23,19 +23,22 @@ if not hasattr(lib, "vasr_diag_rows_stamps"):
 lib.vasr_diag_rows_stamps.argtypes = [ctypes.c_void_p]
 Ms = [int(v) for v in sys.argv[1:]] or [8016, 16032]
 g0 = torch.Generator(device="cuda").manual_seed(0)
-w = torch.randn(1280, 192, device="cuda", generator=g0) * 0.07
-b = torch.cat([torch.zeros(896, device="cuda"), torch.randn(384, device="cuda", generator=g0) * 0.1])
+# ROWS_N=896: the z-in-tail projection (x | B | C | dt, softplus from 512); default the 1280-column form
+NC = int(os.environ.get("ROWS_N", "1280"))
+NOUT = NC - 384
+w = torch.randn(NC, 192, device="cuda", generator=g0) * 0.07
+b = torch.cat([torch.zeros(NOUT, device="cuda"), torch.randn(384, device="cuda", generator=g0) * 0.1])
 buf = torch.zeros(256 * 8 * 8, device="cuda", dtype=torch.int64)
 NAMES = ("wait", "barrier", "epilogue", "dma", "mfma")
 for M in Ms:
     u = torch.randn(M, 192, device="cuda", generator=g0)
-    out = torch.empty(M, 1280, device="cuda")
+    out = torch.empty(M, NC, device="cuda")
     for _ in range(5):
-        ops.gemm(u, w, b, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=896, out=out)
+        ops.gemm(u, w, b, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=NOUT, out=out)
     torch.cuda.synchronize()
     buf.zero_()
     assert lib.vasr_diag_rows_stamps(ctypes.c_void_p(buf.data_ptr())) == 0
-    ops.gemm(u, w, b, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=896, out=out)
+    ops.gemm(u, w, b, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=NOUT, out=out)
     torch.cuda.synchronize()
     assert lib.vasr_diag_rows_stamps(ctypes.c_void_p(0)) == 0
     st = buf.view(-1, 8).cpu()

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Interleaved launch-time A/B of vasr_linear_x3_f32 between library builds of the same ABI (ctypes
+only): the model's K = 192 projection shapes, `reps` back-to-back launches between one HIP event pair
+per library and round, library order rotated every round after a warm-up, every library's C checked
+bitwise against the first's.
+    python tools/gemm_ab_libs.py <rounds> <M:N:n_out,...> lib_a.so lib_b.so ...
+(n_out > 0: softplus from column n_out, the composed projection's epilogue; 0: none)"""
+import ctypes
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "velocity-asr_amd"))
+import torch  # noqa: E402
+
+from velocity_asr._lib import GemmArgs, EPI_NONE, EPI_SOFTPLUS_FROM  # noqa: E402  (struct layout only)
+
+c_p, c_i64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+
+
+def main():
+    rounds = int(sys.argv[1])
+    shapes = [tuple(int(v) for v in s.split(":")) for s in sys.argv[2].split(",")]
+    libs = sys.argv[3:]
+    K, reps = 192, 20
+    g0 = torch.Generator(device="cuda").manual_seed(0)
+    entries = []
+    for path in libs:
+        lib = ctypes.CDLL(path)
+        lib.vasr_linear_x3_f32.argtypes = [ctypes.POINTER(GemmArgs), c_p, c_p]
+        lib.vasr_split_weights_bf16x3.argtypes = [c_p, c_i64, c_int, c_int, c_p, c_p]
+        lib.vasr_split_weights_elems.argtypes = [c_int, c_int]
+        lib.vasr_split_weights_elems.restype = c_i64
+        entries.append([os.path.basename(path), lib, {}])
+    data = {}
+    for M, N, n_out in shapes:
+        w = torch.randn(N, K, device="cuda", generator=g0) * 0.07
+        b = torch.randn(N, device="cuda", generator=g0) * 0.1
+        a = torch.randn(M, K, device="cuda", generator=g0)
+        c = torch.empty(M, N, device="cuda")
+        data[(M, N, n_out)] = (w, b, a, c)
+        for e in entries:
+            planes = torch.empty(int(e[1].vasr_split_weights_elems(N, K)), device="cuda", dtype=torch.int16)
+            assert e[1].vasr_split_weights_bf16x3(w.data_ptr(), K, N, K, planes.data_ptr(), None) == 0
+            args = GemmArgs()
+            args.A, args.lda, args.stride_a = a.data_ptr(), K, 0
+            args.W, args.ldw = w.data_ptr(), K
+            args.bias = b.data_ptr()
+            args.C, args.ldc, args.stride_c = c.data_ptr(), N, 0
+            args.batch, args.M, args.N, args.K = 1, M, N, K
+            args.epilogue = EPI_SOFTPLUS_FROM if n_out else EPI_NONE
+            args.n_out = n_out
+            e[2][(M, N, n_out)] = (args, planes)
+
+    def launch(e, key):
+        args, planes = e[2][key]
+        return e[1].vasr_linear_x3_f32(ctypes.byref(args), ctypes.c_void_p(planes.data_ptr()), None)
+    for key in data:
+        ref = None
+        for e in entries:
+            assert launch(e, key) == 0
+            torch.cuda.synchronize()
+            o = data[key][3].clone()
+            if ref is None:
+                ref = o
+            elif not torch.equal(o, ref):
+                print(f"MISMATCH {e[0]} {key}: max |diff| {(o - ref).abs().max().item():.3e}", flush=True)
+    k0 = next(iter(data))
+    t_end = time.time() + float(os.environ.get("AB_WARM_S", "3"))
+    while time.time() < t_end:
+        for _ in range(20):
+            launch(entries[0], k0)
+        torch.cuda.synchronize()
+    res = {}
+    for r in range(rounds):
+        for key in data:
+            for e in entries[r % len(entries):] + entries[:r % len(entries)]:
+                for _ in range(3):
+                    launch(e, key)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(reps):
+                    launch(e, key)
+                b.record()
+                torch.cuda.synchronize()
+                res.setdefault((e[0], key), []).append(a.elapsed_time(b) * 1e3 / reps)
+    for key in data:
+        for e in entries:
+            v = sorted(res[(e[0], key)])
+            print(f"M={key[0]} N={key[1]} n_out={key[2]} {e[0]:24s} median {v[len(v) // 2]:7.2f} us  best {v[0]:7.2f}  "
+                  f"all {' '.join(f'{t:.1f}' for t in res[(e[0], key)])}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
