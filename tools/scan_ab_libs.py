@@ -4,6 +4,7 @@ ABI >= 12): `reps` back-to-back launches between one HIP event pair per library 
 (B, L) shapes given as B:L, mode 2, Di 384, N 64.
     python tools/scan_ab_libs.py <rounds> <B:L,B:L,...> lib_a.so lib_b.so ..."""
 import ctypes
+import os
 import sys
 
 import torch
@@ -18,7 +19,8 @@ def main():
     for spec in libs:  # path[@key=value]: vasr_set_option(key, value) before each of this entry's launches
         p, _, opt = spec.partition("@")
         lib = ctypes.CDLL(p)
-        f = lib.vasr_ssm_scan_f32
+        # SCAN_UNGATED=1: the z-in-tail blocks' ungated scan (same arguments; reads only x of xz)
+        f = lib.vasr_ssm_scan_ungated_f32 if os.environ.get("SCAN_UNGATED") == "1" else lib.vasr_ssm_scan_f32
         c_p, c_i64 = ctypes.c_void_p, ctypes.c_int64
         f.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p]
         if opt:
