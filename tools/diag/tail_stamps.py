@@ -24,7 +24,7 @@ def main():
     from velocity_asr import _lib, ops
     lib = _lib.lib()
     nblk = (M + 31) // 32
-    stamps = torch.zeros(12 * nblk, device="cuda", dtype=torch.int64)
+    stamps = torch.zeros(16 * nblk, device="cuda", dtype=torch.int64)
     f = lib.vasr_diag_tail_stamps
     f.argtypes = [ctypes.c_void_p]
     assert f(ctypes.c_void_p(stamps.data_ptr())) == 0
@@ -50,13 +50,15 @@ def main():
         e.record()
         torch.cuda.synchronize()
         print(f"round {rnd}: {s.elapsed_time(e) / reps * 1e3:.2f} us per launch", flush=True)
-    st = stamps.view(nblk, 12).cpu().numpy()
-    t = st[:, 3:].astype(np.float64)
-    clock = (t[:, 8] - t[:, 0]) / ((st[:, 2] - st[:, 1]) / 100.0) / 1e3  # GHz (realtime: 100 MHz)
-    names = ["u staged", "z product", "gate+consts", "barrier", "out_proj+LN", "FFN1", "FFN2", "store"]
+    st = stamps.view(nblk, 16).cpu().numpy()
+    order = [0, 1, 2, 3, 4, 9, 10, 5, 11, 6, 7, 8]  # slots in time order
+    t = st[:, 3:15].astype(np.float64)[:, order]
+    clock = (t[:, -1] - t[:, 0]) / ((st[:, 2] - st[:, 1]) / 100.0) / 1e3  # GHz (realtime: 100 MHz)
+    names = ["u staged", "z product", "gate+consts", "barrier", "out_proj", "x1 scratch", "LayerNorm",
+             "FFN1 half 0", "FFN1 half 1", "FFN2", "store"]
     print(f"M={M} {'bf16' if bf16 else 'f32'}: {nblk} workgroups, clock median {np.median(clock):.3f} GHz")
     dur = np.diff(t, axis=1)
-    tot = t[:, 8] - t[:, 0]
+    tot = t[:, -1] - t[:, 0]
     print("phase            median cycles   share")
     for i, n in enumerate(names):
         print(f"{n:16s} {np.median(dur[:, i]):10.0f}   {np.median(dur[:, i]) / np.median(tot):6.3f}")

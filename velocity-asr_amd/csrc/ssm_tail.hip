@@ -111,13 +111,14 @@ struct TailCtx {
     float x1[RT][CT][4];     // residual x, then x1 = out_proj(g) + x
     float bb1[2][CT], bb2[CT], lnw[3], lnb[3];
 #ifdef VASR_TAIL_STAMPS
-    uint64_t ts[10];  // diagnostic builds: s_memtime at the phase boundaries (wave 0)
+    uint64_t ts[13];  // diagnostic builds: s_memtime at the phase boundaries (wave 0)
 #endif
 };
 
 #ifdef VASR_TAIL_STAMPS
 // Diagnostic builds only (-DVASR_TAIL_STAMPS, tools/diag/tail_stamps.py): per workgroup of the gated
-// tail, 12 int64: HW_ID | XCC << 32, s_memrealtime at entry and exit, s_memtime at 9 phase boundaries.
+// tail, 16 int64: HW_ID | XCC << 32, s_memrealtime at entry and exit, s_memtime at 12 phase boundaries
+// (slots 9-11: inside the tail steps, tools/diag/tail_stamps.py orders them).
 __device__ int64_t* g_tail_stamps;
 #define TAIL_STAMP(c, i) ((c).ts[i] = __builtin_amdgcn_s_memtime())
 #else
@@ -207,6 +208,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
     if constexpr (S == 11) {
         // x1 = out_proj(g) + x (registers, kept for the final residual) -> fp32 scratch in R
         // (the g planes are dead once every wave is past its last GEMM1 read)
+        TAIL_STAMP(c, 9);
         lds_barrier();
         float* xs = reinterpret_cast<float*>(c.R);
 #pragma unroll
@@ -222,6 +224,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
                 c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         lds_barrier();
+        TAIL_STAMP(c, 10);
         // h = LayerNorm_2(x1): one wave per row with vasr_layer_norm_f32's operations, each
         // value split into the three planes of H
         for (int rr = c.wave; rr < Ctx::ROWS; rr += Ctx::NWV) {
@@ -261,6 +264,7 @@ __device__ __forceinline__ void tail_step(TailCtx<NP, RT, CT>& c) {
                                 gelu_fast(c.acc[tm][t][i] + c.bb1[hh][t]));
                 c.acc[tm][t] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
+        if constexpr (S == 17) TAIL_STAMP(c, 11);
         if constexpr (S == 23) {
             lds_barrier();  // f complete before FFN2 reads it
             TAIL_STAMP(c, 6);
@@ -576,12 +580,12 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
         uint32_t xcc, hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        int64_t* o = g_tail_stamps + 12 * (int64_t)blockIdx.x;
+        int64_t* o = g_tail_stamps + 16 * (int64_t)blockIdx.x;
         o[0] = (int64_t)hw | ((int64_t)(xcc & 0xF) << 32);
         o[1] = (int64_t)rt0;
         o[2] = (int64_t)rt1;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) o[3 + i] = (int64_t)c.ts[i];
+        for (int i = 0; i < 12; ++i) o[3 + i] = (int64_t)c.ts[i];
     }
 #endif
 }
