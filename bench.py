@@ -215,12 +215,15 @@ def isolated_times(model, audio, reps=20):
             from velocity_asr.ssm import _tree_mode
             Di, N = blk.ssm.d_inner, blk.ssm.state_dim
             mode = _tree_mode()
-            if "w_noz" in p:  # fp32: one projection GEMM writes [x | B | C | dt]
-                proj = lambda: ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM,  # noqa: E731
+            from velocity_asr.ssm import _bf16_compose
+            wn = "w_noz" if "w_noz" in p else "w_noz16" if ("w_noz16" in p and _bf16_compose()) else None
+            if wn:  # one projection GEMM writes [x | B | C | dt] (fp32, or the bf16 model's composed form)
+                bn = "b_noz" if wn == "w_noz" else "b_noz16"
+                proj = lambda: ops.gemm(u, p[wn], p[bn], epilogue=_lib.EPI_SOFTPLUS_FROM,  # noqa: E731
                                         n_out=Di + 2 * N)
                 xbd = proj()
                 xs, bc, dt = xbd[:, :Di], xbd[:, Di:Di + 2 * N], xbd[:, Di + 2 * N:]
-                out = dict(gemm=per_launch(proj), gemm_key=(B * L, p["w_noz"].shape[0], D, 1))
+                out = dict(gemm=per_launch(proj), gemm_key=(B * L, p[wn].shape[0], D, 1))
             else:  # bf16: in_proj's x rows, then [x_proj; dt_proj]
                 xs = ops.gemm(u, p["w_x"])
                 xdt = ops.gemm(xs, p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=2 * N)

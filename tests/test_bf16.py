@@ -105,3 +105,22 @@ def test_bf16_graphed_transcriber(va, model_bf16):
     gt.step()
     torch.cuda.synchronize()
     assert token_lists(gt.tokens, gt.lengths) == token_lists(te, le)
+
+
+def test_composed_projection_bf16(va, monkeypatch):
+    """The bf16 model's composed projection ([W_in; W_xdt W_in,x] as one bf16 GEMM, the default) vs the
+    two GEMMs (VASR_BF16_COMPOSE=0): x and z are the same GEMM columns (bitwise), B | C | dt differ by
+    one bf16 rounding of the composed weight instead of one of x_p (bf16 tolerance)."""
+    W = S.make_weights(None, seed=0)
+    m = va.VELOCITYASR()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
+    ssm = m.to(DEV).to(torch.bfloat16).eval().local_ssm.layers[3].ssm
+    u = torch.from_numpy(np.random.default_rng(11).standard_normal((600, 192)).astype(np.float32)).to(DEV)
+    monkeypatch.setenv("VASR_BF16_COMPOSE", "1")
+    xz1, xdt1 = ssm.project(u)
+    monkeypatch.setenv("VASR_BF16_COMPOSE", "0")
+    xz0, xdt0 = ssm.project(u)
+    assert torch.equal(xz1, xz0)
+    err = (xdt1 - xdt0).abs().max().item()
+    scale = xdt0.abs().max().item()
+    assert err <= 2e-2 * scale, (err, scale)

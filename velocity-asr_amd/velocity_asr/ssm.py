@@ -45,6 +45,12 @@ def _tree_mode() -> int:
 _warned_training = False
 
 
+def _bf16_compose() -> bool:
+    """The bf16 model's composed projection (SelectiveSSM._prepared); VASR_BF16_COMPOSE=0 selects
+    the two GEMMs (read per call so tests can compare the two)."""
+    return os.environ.get("VASR_BF16_COMPOSE", "1") != "0"
+
+
 def _check_eval(module: nn.Module) -> None:
     global _warned_training
     if module.training and not _warned_training:
@@ -111,6 +117,15 @@ class SelectiveSSM(nn.Module):
                 Di = self.d_inner
                 out["w_x"] = self.in_proj.weight.detach()[:Di].contiguous()
                 out["w_z"] = self.in_proj.weight.detach()[Di:].contiguous()
+                # composed form (default; VASR_BF16_COMPOSE=0: the two GEMMs): [W_in; W_xdt W_in,x] as
+                # one bf16 GEMM, the product of the bf16 weights formed in float64 and rounded to bf16
+                # once -- one bf16 rounding where the two GEMMs round x_p to bf16 at the second
+                # GEMM's input (C3's token edit rate vs the reference 2.28 % vs 2.31 %, profiles/r06ad/)
+                wc = (w.detach().double() @ out["w_x"].double()).to(torch.bfloat16)
+                out["w_comb16"] = torch.cat([self.in_proj.weight.detach(), wc], 0).contiguous()
+                out["b_comb16"] = torch.cat([torch.zeros(2 * Di, device=dev), b]).contiguous()
+                out["w_noz16"] = torch.cat([out["w_x"], wc], 0).contiguous()
+                out["b_noz16"] = torch.cat([torch.zeros(Di, device=dev), b]).contiguous()
             return out
         return cached(self, "ssm", (self.x_proj.weight, self.dt_proj.weight, self.dt_proj.bias, self.A_log,
                                     self.in_proj.weight), build)
@@ -136,6 +151,9 @@ class SelectiveSSM(nn.Module):
         if "w_comb" in p and os.environ.get("VASR_XDT_COMPOSE", "1") != "0":
             out = ops.gemm(u, p["w_comb"], p["b_comb"], epilogue=_lib.EPI_SOFTPLUS_FROM,
                            n_out=2 * Di + 2 * N)                                 # (M, 2Di + 2N + Di)
+            return out[:, :2 * Di], out[:, 2 * Di:]
+        if "w_comb16" in p and _bf16_compose():  # the bf16 model's composed form (see _prepared)
+            out = ops.gemm(u, p["w_comb16"], p["b_comb16"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=2 * Di + 2 * N)
             return out[:, :2 * Di], out[:, 2 * Di:]
         xz = ops.gemm(u, self.in_proj.weight)                                   # (M, 2Di) [x | z]
         xdt = ops.gemm(xz[:, :Di], p["w_xdt"], p["b_xdt"], epilogue=_lib.EPI_SOFTPLUS_FROM,
@@ -236,8 +254,9 @@ class SSMBlock(nn.Module):
         x2 = x.view(B * L, D)
         u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
                           self.conv.bias, self.norm1.eps).view(B * L, D)
-        if "w_noz" in p:
-            xbd = ops.gemm(u, p["w_noz"], p["b_noz"], epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=Di + 2 * N)  # [x|B|C|dt]
+        if "w_noz" in p or ("w_noz16" in p and _bf16_compose()):
+            w, b = (p["w_noz"], p["b_noz"]) if "w_noz" in p else (p["w_noz16"], p["b_noz16"])
+            xbd = ops.gemm(u, w, b, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=Di + 2 * N)  # [x|B|C|dt]
             xs, bc, dt = xbd[:, :Di], xbd[:, Di:Di + 2 * N], xbd[:, Di + 2 * N:]
         else:
             xs = ops.gemm(u, p["w_x"])                                                 # (M, Di) x
