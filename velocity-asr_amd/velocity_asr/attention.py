@@ -96,8 +96,11 @@ class MultiHeadAttention(nn.Module):
         return cached(self, "kv", Q.deps(self.k_proj) + Q.deps(self.v_proj), build)
 
     def forward(self, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor,
-                mask: Optional[torch.Tensor] = None, key_lengths: Optional[Sequence[int]] = None) -> torch.Tensor:
-        """key_lengths: per-utterance valid keys of a padded (B, Kp, D) key set."""
+                mask: Optional[torch.Tensor] = None, key_lengths: Optional[Sequence[int]] = None,
+                project_out: bool = True) -> torch.Tensor:
+        """key_lengths: per-utterance valid keys of a padded (B, Kp, D) key set.  project_out=False:
+        the (B * Lq, attention_dim) head outputs before out_proj (GatedFusion.forward_attention
+        folds out_proj into its global-branch product)."""
         if mask is not None:
             raise NotImplementedError("velocity_asr (MI355X build): attention masks are not supported "
                                       "(the reference path never passes one)")
@@ -119,6 +122,8 @@ class MultiHeadAttention(nn.Module):
         Q.record(self.v_proj, kv[:, A:])
         o = ops.pooled_attention(q, kv, B, Lq, Kp, self.num_heads,
                                  kps=None if key_lengths is None else _device_ints(key_lengths, q.device))
+        if not project_out:
+            return o
         wo, bo, qpo = Q.linear_parts(self.out_proj)
         out = ops.gemm(o, wo, bo, qparams=qpo)
         Q.record(self.out_proj, out)
@@ -160,6 +165,42 @@ class GatedFusion(nn.Module):
                                 Q.act_qparams_or_identity(loc, D, dev)], 0).contiguous()
             return w_local, w_glob, b_glob, qp
         return cached(self, "paired", Q.deps(gate) + Q.deps(loc) + Q.deps(glob), build)
+
+    def _paired_attention(self, mha: "MultiHeadAttention"):
+        """The global branch with the attention's out_proj folded in: global_context = o Wo^T + bo
+        feeds only this product, so [gate_g | global_proj] (o Wo^T + bo) + b = o ([gate_g |
+        global_proj] Wo)^T + ([gate_g | global_proj] bo + b), the composite formed in float64 and
+        rounded once (as the SSM's composed projection): K = attention_dim (48) instead of d_model,
+        and no (B * L, d_model) global_context in HBM."""
+        _, w_glob, b_glob, _ = self._paired()
+
+        def build():
+            wo, bo = mha.out_proj.weight, mha.out_proj.bias
+            w = (w_glob.detach().double() @ wo.detach().double()).to(w_glob.dtype).contiguous()
+            b = (ops.f32(b_glob).double() + w_glob.detach().double() @ ops.f32(bo).detach().double()).float().contiguous()
+            return w, b
+        return cached(self, "paired_attn", (w_glob, b_glob, mha.out_proj.weight, mha.out_proj.bias), build)
+
+    def composable(self, mha: "MultiHeadAttention") -> bool:
+        """forward_attention applies: plain Linears (no QAT fake-quant on global_context or the
+        fusion's inputs), one weight dtype; VASR_ATTN_COMPOSE=0 keeps the separate out_proj."""
+        import os
+        mods = (mha.out_proj, self.gate_proj[0], self.local_proj, self.global_proj, self.out_proj)
+        return (os.environ.get("VASR_ATTN_COMPOSE", "1") != "0" and all(type(m) is nn.Linear for m in mods)
+                and len({m.weight.dtype for m in mods}) == 1 and mha.out_proj.bias is not None)
+
+    def forward_attention(self, local_features: torch.Tensor, o: torch.Tensor,
+                          mha: "MultiHeadAttention") -> torch.Tensor:
+        """forward(local_features, mha's output) from the attention's head outputs o (B * L, A)."""
+        B, L, D = local_features.shape
+        local2 = local_features.reshape(B * L, D)
+        w_local, _, _, qp = self._paired()
+        w_glob, b_glob = self._paired_attention(mha)
+        t1 = ops.gemm(local2, w_local)
+        fused = ops.gemm(o, w_glob, b_glob, epilogue=_lib.EPI_PAIR_FUSION, aux=t1,
+                         aux2=self.local_proj.bias, n_out=D, qparams=qp)
+        out = ops.gemm(fused, self.out_proj.weight, self.out_proj.bias)
+        return out.view(B, L, D)
 
     def _observe(self, local2: torch.Tensor, glob2: torch.Tensor) -> None:
         """Calibration only: the raw (pre-quantizer) gate / local / global outputs, summed in
@@ -215,6 +256,9 @@ class HierarchicalGlobalContext(nn.Module):
                                          lengths=None if lengths is None else pool_size1)
         x_pool2 = ops.layer_norm(x_pool2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         query = ops.layer_norm(local_features, self.norm2.weight, self.norm2.bias, self.norm2.eps)
-        global_context = self.cross_attention(query=query, key=x_pool2, value=x_pool2,
-                                              key_lengths=None if lengths is None else pool_size2)
+        kl = None if lengths is None else pool_size2
+        if self.fusion.composable(self.cross_attention):
+            o = self.cross_attention(query=query, key=x_pool2, value=x_pool2, key_lengths=kl, project_out=False)
+            return self.fusion.forward_attention(local_features, o, self.cross_attention)
+        global_context = self.cross_attention(query=query, key=x_pool2, value=x_pool2, key_lengths=kl)
         return self.fusion(local_features, global_context)
