@@ -418,6 +418,9 @@ __device__ __forceinline__ void gate_split_store4(char* plane0, int plane_bytes,
 // product of the same bf16 pairs in the same k order), so a lane holds 16 z columns of ONE token in
 // four runs of four: y + x D arrives as four float4 loads and g leaves as one 8-B store per run and
 // plane (instead of 16 scalar loads and 16 x NP two-byte stores); the u tile's loads go first
+#ifndef VASR_TAILG_XCD
+#define VASR_TAILG_XCD 1
+#endif
 #ifndef VASR_TAILG_SWAP
 #define VASR_TAILG_SWAP 1
 #endif
@@ -433,7 +436,18 @@ __global__ __launch_bounds__(768, 1) void ssm_tail_gated_kernel(TailParams P, Ga
     c.wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     c.r = c.lane & 15;
     c.q = c.lane >> 4;
+#if VASR_TAILG_XCD
+    // XCD-aware tile order: workgroups id, id + 8, ... run on one XCD; give each such group a run of
+    // consecutive row tiles, as the scan gives each XCD a run of consecutive utterances
+    // (scan_body.inc), so a tile's y + x D rows were written through the same L2
+    {
+        const int nblk = (int)gridDim.x, id = (int)blockIdx.x;
+        const int q8 = nblk / 8, r8 = nblk % 8, xg = id % 8;
+        c.m0 = ((xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + id / 8) * Ctx::ROWS;
+    }
+#else
     c.m0 = blockIdx.x * Ctx::ROWS;
+#endif
 #ifdef VASR_TAIL_STAMPS
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
