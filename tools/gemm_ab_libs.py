@@ -3,7 +3,7 @@
 only): the model's K = 192 projection shapes, `reps` back-to-back launches between one HIP event pair
 per library and round, library order rotated every round after a warm-up, every library's C checked
 bitwise against the first's.
-    python tools/gemm_ab_libs.py <rounds> <M:N:n_out,...> lib_a.so lib_b.so ...
+    python tools/gemm_ab_libs.py <rounds> <M:N:n_out[:K],...> lib_a.so lib_b.so ...  (K default 192)
 (n_out > 0: softplus from column n_out, the composed projection's epilogue; 0: none; -1: the argmax
 head's keys, VASR_EPI_ARGMAX)"""
 import ctypes
@@ -23,7 +23,7 @@ def main():
     rounds = int(sys.argv[1])
     shapes = [tuple(int(v) for v in s.split(":")) for s in sys.argv[2].split(",")]
     libs = sys.argv[3:]
-    K, reps = 192, 20
+    reps = 20
     g0 = torch.Generator(device="cuda").manual_seed(0)
     entries = []
     for path in libs:
@@ -34,13 +34,15 @@ def main():
         lib.vasr_split_weights_elems.restype = c_i64
         entries.append([os.path.basename(path), lib, {}])
     data = {}
-    for M, N, n_out in shapes:
+    for shp in shapes:
+        M, N, n_out = shp[:3]
+        K = shp[3] if len(shp) > 3 else 192
         w = torch.randn(N, K, device="cuda", generator=g0) * 0.07
         b = torch.randn(N, device="cuda", generator=g0) * 0.1
         a = torch.randn(M, K, device="cuda", generator=g0)
         slots = (N + 31) // 32
         c = torch.empty(M, slots, device="cuda", dtype=torch.int64) if n_out < 0 else torch.empty(M, N, device="cuda")
-        data[(M, N, n_out)] = (w, b, a, c)
+        data[shp] = (w, b, a, c)
         for e in entries:
             planes = torch.empty(int(e[1].vasr_split_weights_elems(N, K)), device="cuda", dtype=torch.int16)
             assert e[1].vasr_split_weights_bf16x3(w.data_ptr(), K, N, K, planes.data_ptr(), None) == 0
@@ -52,7 +54,7 @@ def main():
             args.batch, args.M, args.N, args.K = 1, M, N, K
             args.epilogue = EPI_ARGMAX if n_out < 0 else EPI_SOFTPLUS_FROM if n_out else EPI_NONE
             args.n_out = max(n_out, 0)
-            e[2][(M, N, n_out)] = (args, planes)
+            e[2][shp] = (args, planes)
 
     def launch(e, key):
         args, planes = e[2][key]
@@ -91,7 +93,7 @@ def main():
     for key in data:
         for e in entries:
             v = sorted(res[(e[0], key)])
-            print(f"M={key[0]} N={key[1]} n_out={key[2]} {e[0]:24s} median {v[len(v) // 2]:7.2f} us  best {v[0]:7.2f}  "
+            print(f"M={key[0]} N={key[1]} n_out={key[2]} K={key[3] if len(key) > 3 else 192} {e[0]:24s} median {v[len(v) // 2]:7.2f} us  best {v[0]:7.2f}  "
                   f"all {' '.join(f'{t:.1f}' for t in res[(e[0], key)])}", flush=True)
 
 
