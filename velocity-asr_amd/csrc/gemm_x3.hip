@@ -398,6 +398,10 @@ static long x3_min_tiles(int cfg) {
 
 int pick_x3(int M, int N, int batch, bool pair) {
     for (int i = 0; i < 2; ++i) {
+        // N <= 192 (three 64-column tiles or fewer): 64 x 64 tiles at any M (the temporal binding and
+        // the fusion's out_proj at M = 16032: 15.7 vs 16.7 and 12.9 vs 13.9 us for 128 x 64,
+        // profiles/r06an/)
+        if (i == 1 && N <= 192 && !pair) break;
         const TileCfg& c = kCfgs[i];
         const long tiles = (long)((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn()) * batch;
         const bool exact_n = N % c.bn() == 0 || N > 4 * c.bn();  // little padding waste
