@@ -26,13 +26,16 @@ def main():
     reps = 20
     g0 = torch.Generator(device="cuda").manual_seed(0)
     entries = []
-    for path in libs:
+    for spec in libs:  # path[@key=value]: vasr_set_option(key, value) before each of this entry's launches
+        path, _, opt = spec.partition("@")
         lib = ctypes.CDLL(path)
+        lib.vasr_set_option.argtypes = [c_int, c_int]
         lib.vasr_linear_x3_f32.argtypes = [ctypes.POINTER(GemmArgs), c_p, c_p]
         lib.vasr_split_weights_bf16x3.argtypes = [c_p, c_i64, c_int, c_int, c_p, c_p]
         lib.vasr_split_weights_elems.argtypes = [c_int, c_int]
         lib.vasr_split_weights_elems.restype = c_i64
-        entries.append([os.path.basename(path), lib, {}])
+        entries.append([os.path.basename(path) + (f"@{opt}" if opt else ""), lib, {},
+                        tuple(int(v) for v in opt.split("=")) if opt else None])
     data = {}
     for shp in shapes:
         M, N, n_out = shp[:3]
@@ -58,6 +61,8 @@ def main():
 
     def launch(e, key):
         args, planes = e[2][key]
+        if e[3]:
+            assert e[1].vasr_set_option(*e[3]) >= 0
         return e[1].vasr_linear_x3_f32(ctypes.byref(args), ctypes.c_void_p(planes.data_ptr()), None)
     for key in data:
         ref = None
