@@ -14,7 +14,7 @@ def main():
     rounds = int(sys.argv[1])
     shapes = [tuple(int(v) for v in s.split(":")) for s in sys.argv[2].split(",")]
     libs = sys.argv[3:]
-    Di, N, reps = 384, 64, 20
+    Di, N, reps = 384, int(os.environ.get("SCAN_N", "64")), 20
     fns = []
     for spec in libs:  # path[@key=value]: vasr_set_option(key, value) before each of this entry's launches
         p, _, opt = spec.partition("@")
