@@ -26,6 +26,9 @@ def main():
     reps = 20
     g0 = torch.Generator(device="cuda").manual_seed(0)
     entries = []
+    # every option key any entry sets is set by every entry (0 = default where the entry names none): the
+    # same library loaded twice is one handle, so an option would otherwise carry over to the next entry
+    keys = sorted({int(s.partition("@")[2].split("=")[0]) for s in libs if "@" in s})
     for spec in libs:  # path[@key=value]: vasr_set_option(key, value) before each of this entry's launches
         path, _, opt = spec.partition("@")
         lib = ctypes.CDLL(path)
@@ -34,8 +37,9 @@ def main():
         lib.vasr_split_weights_bf16x3.argtypes = [c_p, c_i64, c_int, c_int, c_p, c_p]
         lib.vasr_split_weights_elems.argtypes = [c_int, c_int]
         lib.vasr_split_weights_elems.restype = c_i64
+        mine = dict([tuple(int(v) for v in opt.split("="))]) if opt else {}
         entries.append([os.path.basename(path) + (f"@{opt}" if opt else ""), lib, {},
-                        tuple(int(v) for v in opt.split("=")) if opt else None])
+                        tuple((k, mine.get(k, 0)) for k in keys)])
     data = {}
     for shp in shapes:
         M, N, n_out = shp[:3]
@@ -61,8 +65,8 @@ def main():
 
     def launch(e, key):
         args, planes = e[2][key]
-        if e[3]:
-            assert e[1].vasr_set_option(*e[3]) >= 0
+        for k, v in e[3]:
+            assert e[1].vasr_set_option(k, v) >= 0
         return e[1].vasr_linear_x3_f32(ctypes.byref(args), ctypes.c_void_p(planes.data_ptr()), None)
     for key in data:
         ref = None

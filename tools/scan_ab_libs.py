@@ -16,6 +16,9 @@ def main():
     libs = sys.argv[3:]
     Di, N, reps = 384, int(os.environ.get("SCAN_N", "64")), 20
     fns = []
+    # every option key any entry sets is set by every entry (0 = the launcher's default where the entry
+    # names none): the same library loaded twice is one handle, so an option would otherwise carry over
+    keys = sorted({int(s.partition("@")[2].split("=")[0]) for s in libs if "@" in s})
     for spec in libs:  # path[@key=value]: vasr_set_option(key, value) before each of this entry's launches
         p, _, opt = spec.partition("@")
         lib = ctypes.CDLL(p)
@@ -23,12 +26,13 @@ def main():
         f = lib.vasr_ssm_scan_ungated_f32 if os.environ.get("SCAN_UNGATED") == "1" else lib.vasr_ssm_scan_f32
         c_p, c_i64 = ctypes.c_void_p, ctypes.c_int64
         f.argtypes = [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p]
-        if opt:
-            key, val = (int(v) for v in opt.split("="))
+        if keys:
+            mine = dict([tuple(int(v) for v in opt.split("="))]) if opt else {}
             lib.vasr_set_option.argtypes = [ctypes.c_int, ctypes.c_int]
 
-            def f(*a, _f=f, _lib=lib, _k=key, _v=val):
-                assert _lib.vasr_set_option(_k, _v) >= 0
+            def f(*a, _f=f, _lib=lib, _kv=tuple((k, mine.get(k, 0)) for k in keys)):
+                for k, v in _kv:
+                    assert _lib.vasr_set_option(k, v) >= 0
                 return _f(*a)
         fns.append((spec.split("/")[-1], f))
     data = {}
