@@ -119,7 +119,13 @@ __global__ __launch_bounds__(256) void mel_chunk_log_kernel(const float* __restr
     __shared__ int rp_s[kMaxMels + 1];
     __shared__ int col_s[kMaxNnz];
     __shared__ float val_s[kMaxNnz];
-    const int b = blockIdx.y, c = blockIdx.x, nch = gridDim.x;
+    const int nch = gridDim.x;
+    int b = blockIdx.y, c = blockIdx.x;
+    if (VASR_FE_XCD & 2) {  // the STFT's (b, frame) runs per XCD: its power rows are read from this L2
+        const int w = xcd_run(c + b * nch, nch * (int)gridDim.y);
+        b = w / nch;
+        c = w - b * nch;
+    }
     const int f0 = c * kFC;
     const int nf = min(kFC, F - f0);
     const int nnz = rowptr[n_mels];
@@ -244,7 +250,12 @@ __global__ __launch_bounds__(256) void mel_chunk_norm_kernel(const float* __rest
                                                              int64_t out_stride, int frame_off, int F, int n_mels,
                                                              int normalize, const int32_t* __restrict__ frames) {
     __shared__ float st_s[2 * kMaxMels];
-    const int b = blockIdx.y, c = blockIdx.x;
+    int b = blockIdx.y, c = blockIdx.x;
+    if (VASR_FE_XCD & 4) {  // the log pass's runs: its log-mel rows are read from this L2
+        const int w = xcd_run(c + b * (int)gridDim.x, (int)(gridDim.x * gridDim.y));
+        b = w / (int)gridDim.x;
+        c = w - b * (int)gridDim.x;
+    }
     const int f0 = c * kFC;
     const int nf = min(kFC, F - f0);
     const int nv = frames ? max(min(nf, frames[b] - f0), 0) : nf;  // frames past the utterance's end -> 0

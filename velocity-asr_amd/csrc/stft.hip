@@ -133,7 +133,13 @@ __global__ __launch_bounds__(256) void stft_power_400_kernel(const float* __rest
     __shared__ cf tw[kHalf + kBins];  // W200^j, then W400^k
     __shared__ cf za[FPB][kHalf];
     __shared__ cf zb[FPB][kHalf];
-    const int b = blockIdx.y, f0 = blockIdx.x * FPB;
+    int b = blockIdx.y, fb = blockIdx.x;
+    if (VASR_FE_XCD & 1) {  // (b, frame-block) runs per XCD, as the mel pass reads them
+        const int w = xcd_run(fb + b * (int)gridDim.x, (int)(gridDim.x * gridDim.y));
+        b = w / (int)gridDim.x;
+        fb = w - b * (int)gridDim.x;
+    }
+    const int f0 = fb * FPB;
     const int tid = threadIdx.x;
     const float* ab = audio + (int64_t)b * ld_audio;
     // 1. windowed even / odd sample pairs packed as complex, straight from the unpadded audio

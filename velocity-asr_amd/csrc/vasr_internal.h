@@ -40,6 +40,17 @@ int mel_chunk_finish(float* workspace, float* out, int64_t out_stride, int frame
 
 constexpr int kWave = 64;
 
+#ifndef VASR_FE_XCD
+#define VASR_FE_XCD 0  // front end XCD-run block order, bit mask: 1 STFT, 2 log-mel, 4 norm (r06ay: off)
+#endif
+// Workgroups id, id + 8, id + 16, ... are dealt to the same XCD (round-robin dispatch); the
+// returned work index gives each XCD a contiguous run of the n work items, so neighbouring
+// items (and a consumer kernel mapped the same way) share that XCD's L2.
+__device__ __forceinline__ int xcd_run(int id, int n) {
+    const int q8 = n / 8, r8 = n % 8, xg = id % 8;
+    return (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + id / 8;
+}
+
 // Sum over the 64 lanes, broadcast to all: DPP within and across 16-lane rows (no LDS
 // round trips, unlike a ds_bpermute butterfly): row sums by quad_perm / half-mirror / mirror,
 // then row_bcast15 / row_bcast31 chain the rows into lane 63, read back as a scalar.
