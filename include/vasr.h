@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 16
+#define VASR_ABI_VERSION 17
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -145,6 +145,15 @@ int64_t vasr_pack_weights_bf16_elems(int N, int K);
  */
 int vasr_layer_norm_f32(const float* x, int64_t ldx, const float* w, const float* b,
                         float* y, int64_t ldy, int rows, int C, float eps, void* stream);
+
+/* Two LayerNorms in a row, one launch: y1 = LN(x; w1, b1, eps1), y2 = LN(y1; w2, b2, eps2), each
+ * bitwise what vasr_layer_norm_f32 gives (y2 from y1's registers, not re-read).  Replaces the
+ * local stack's final norm (LocalSSMProcessor.norm, reference ssm.py:504) followed by the
+ * global context's query norm (HierarchicalGlobalContext.norm2, attention.py:307), which the
+ * reference runs as two nn.LayerNorm calls.  y1 != y2; C <= 1024. */
+int vasr_layer_norm_pair_f32(const float* x, int64_t ldx, const float* w1, const float* b1, float eps1,
+                             float* y1, int64_t ldy1, const float* w2, const float* b2, float eps2,
+                             float* y2, int64_t ldy2, int rows, int C, void* stream);
 
 /* out[b][l][c] = x[b][l][c] + table[l][c] for x (B, L, C) contiguous (standalone
  * PositionalEncoding2D.forward, model.py:106-127; the model fuses it into the conv GEMM). */

@@ -17,18 +17,16 @@ constexpr int kMaxPerLane = 16;  // C <= 1024
 // same values in the same order (the generic path's extra terms are exact zeros), so the
 // result is bitwise the same.
 template <int CPL>
-__device__ __forceinline__ void ln_row_to(const float* __restrict__ x, const float* __restrict__ w,
-                                          const float* __restrict__ b, float* __restrict__ y, int C,
-                                          float eps, int lane) {
-    constexpr int PL = CPL > 0 ? CPL : kMaxPerLane;
-    float v[PL];
+constexpr int ln_per_lane() { return CPL > 0 ? CPL : kMaxPerLane; }
+
+// v[i] = column i * 64 + lane of one row (0 past C) -> its LayerNorm, in place (0 past C).
+template <int CPL>
+__device__ __forceinline__ void ln_vals(float (&v)[ln_per_lane<CPL>()], const float* __restrict__ w,
+                                        const float* __restrict__ b, int C, float eps, int lane) {
+    constexpr int PL = ln_per_lane<CPL>();
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
-        const int c = i * 64 + lane;
-        v[i] = (CPL > 0 || c < C) ? x[c] : 0.f;
-        s += v[i];
-    }
+    for (int i = 0; i < PL; ++i) s += v[i];
     const float mean = wave_sum(s) / (float)C;
     float q = 0.f;
 #pragma unroll
@@ -42,7 +40,30 @@ __device__ __forceinline__ void ln_row_to(const float* __restrict__ x, const flo
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
         const int c = i * 64 + lane;
-        if (CPL > 0 || c < C) y[c] = __builtin_fmaf((v[i] - mean) * rstd, w[c], b[c]);  // as the GEMM LN prologue
+        v[i] = (CPL > 0 || c < C) ? __builtin_fmaf((v[i] - mean) * rstd, w[c], b[c]) : 0.f;  // as the GEMM LN prologue
+    }
+}
+
+// CPL: floats per lane as a compile-time constant when C = 64 * CPL (the model's C = 192 is
+// CPL = 3), so every load and store is unguarded and all of a row's loads issue before the
+// first reduction; CPL = 0 is the generic path (C <= 1024, per-element guards).  Both add the
+// same values in the same order (the generic path's extra terms are exact zeros), so the
+// result is bitwise the same.
+template <int CPL>
+__device__ __forceinline__ void ln_load(float (&v)[ln_per_lane<CPL>()], const float* __restrict__ x, int C, int lane) {
+#pragma unroll
+    for (int i = 0; i < ln_per_lane<CPL>(); ++i) {
+        const int c = i * 64 + lane;
+        v[i] = (CPL > 0 || c < C) ? x[c] : 0.f;
+    }
+}
+
+template <int CPL>
+__device__ __forceinline__ void ln_store(const float (&v)[ln_per_lane<CPL>()], float* __restrict__ y, int C, int lane) {
+#pragma unroll
+    for (int i = 0; i < ln_per_lane<CPL>(); ++i) {
+        const int c = i * 64 + lane;
+        if (CPL > 0 || c < C) y[c] = v[i];
     }
 }
 
@@ -53,7 +74,33 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
                                                          int64_t ldy, int rows, int C, float eps) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
-    ln_row_to<CPL>(x + (int64_t)row * ldx, w, b, y + (int64_t)row * ldy, C, eps, threadIdx.x & 63);
+    const int lane = threadIdx.x & 63;
+    float v[ln_per_lane<CPL>()];
+    ln_load<CPL>(v, x + (int64_t)row * ldx, C, lane);
+    ln_vals<CPL>(v, w, b, C, eps, lane);
+    ln_store<CPL>(v, y + (int64_t)row * ldy, C, lane);
+}
+
+// y1 = LN1(x), y2 = LN2(y1): the second LayerNorm from the first's registers (the same floats
+// it stores, so y2 is bitwise what layer_norm_kernel gives on y1), one read of x instead of two
+// launches.  The local stack's final norm and the global context's query norm (attention.py).
+template <int CPL>
+__global__ __launch_bounds__(256) void layer_norm_pair_kernel(const float* __restrict__ x, int64_t ldx,
+                                                              const float* __restrict__ w1,
+                                                              const float* __restrict__ b1, float eps1,
+                                                              float* __restrict__ y1, int64_t ldy1,
+                                                              const float* __restrict__ w2,
+                                                              const float* __restrict__ b2, float eps2,
+                                                              float* __restrict__ y2, int64_t ldy2, int rows, int C) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
+    float v[ln_per_lane<CPL>()];
+    ln_load<CPL>(v, x + (int64_t)row * ldx, C, lane);
+    ln_vals<CPL>(v, w1, b1, C, eps1, lane);
+    ln_store<CPL>(v, y1 + (int64_t)row * ldy1, C, lane);
+    ln_vals<CPL>(v, w2, b2, C, eps2, lane);
+    ln_store<CPL>(v, y2 + (int64_t)row * ldy2, C, lane);
 }
 
 // TT: output rows per block -- 16 for full-chip launches (1024 blocks at B = 32, L = 501: 4 per
@@ -230,6 +277,29 @@ VASR_API int vasr_layer_norm_f32(const float* x, int64_t ldx, const float* w, co
         default: hipLaunchKernelGGL(layer_norm_kernel<0>, grid, block, 0, s, x, ldx, w, b, y, ldy, rows, C, eps); break;
     }
     return launch_status("vasr_layer_norm_f32");
+}
+
+VASR_API int vasr_layer_norm_pair_f32(const float* x, int64_t ldx, const float* w1, const float* b1, float eps1,
+                                      float* y1, int64_t ldy1, const float* w2, const float* b2, float eps2, float* y2,
+                                      int64_t ldy2, int rows, int C, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && w1 && b1 && y1 && w2 && b2 && y2, "vasr_layer_norm_pair_f32: null pointer");
+    VASR_CHECK_ARG(C > 0 && C <= 64 * kMaxPerLane && rows >= 0, "vasr_layer_norm_pair_f32: bad shape rows=%d C=%d",
+                   rows, C);
+    VASR_CHECK_ARG(y1 != y2, "vasr_layer_norm_pair_f32: y1 and y2 must differ");
+    if (rows == 0) return VASR_OK;
+    const dim3 grid((rows + 3) / 4), block(256);
+    hipStream_t s = as_stream(stream);
+#define VASR_LN2(CPL)                                                                                                \
+    hipLaunchKernelGGL(layer_norm_pair_kernel<CPL>, grid, block, 0, s, x, ldx, w1, b1, eps1, y1, ldy1, w2, b2, eps2, \
+                       y2, ldy2, rows, C)
+    switch (C) {
+        case 192: VASR_LN2(3); break;
+        case 384: VASR_LN2(6); break;
+        default: VASR_LN2(0); break;
+    }
+#undef VASR_LN2
+    return launch_status("vasr_layer_norm_pair_f32");
 }
 
 VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b, const float* conv_w,

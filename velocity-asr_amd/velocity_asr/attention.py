@@ -246,16 +246,20 @@ class HierarchicalGlobalContext(nn.Module):
         self.norm2 = nn.LayerNorm(d_model)
         self.fusion = GatedFusion(d_model=d_model)
 
-    def forward(self, local_features: torch.Tensor, lengths: Optional[Sequence[int]] = None) -> torch.Tensor:
+    def forward(self, local_features: torch.Tensor, lengths: Optional[Sequence[int]] = None,
+                query: Optional[torch.Tensor] = None) -> torch.Tensor:
         """lengths: per-utterance token counts of a zero-padded batch (None: all L).  Pooling
         sizes and attention keys then follow each utterance's own length; the global SSM is
-        causal, so the junk rows past an utterance's pooled tokens never reach them."""
+        causal, so the junk rows past an utterance's pooled tokens never reach them.
+        query (extension): norm2(local_features) when the caller already has it
+        (LocalSSMProcessor.forward_pair)."""
         x_pool1, pool_size1 = self.pool1(local_features, lengths=lengths)
         x_ssm = self.global_ssm(x_pool1)
         x_pool2, pool_size2 = self.pool2(x_ssm, prev_pool_size=pool_size1,
                                          lengths=None if lengths is None else pool_size1)
         x_pool2 = ops.layer_norm(x_pool2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
-        query = ops.layer_norm(local_features, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        if query is None:
+            query = ops.layer_norm(local_features, self.norm2.weight, self.norm2.bias, self.norm2.eps)
         kl = None if lengths is None else pool_size2
         if self.fusion.composable(self.cross_attention):
             o = self.cross_attention(query=query, key=x_pool2, value=x_pool2, key_lengths=kl, project_out=False)

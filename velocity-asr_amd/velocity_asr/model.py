@@ -199,6 +199,18 @@ class VELOCITYASR(nn.Module):
             raise ValueError(f"frames: each utterance needs 1..{n_frames} frames, got {frames}")
         return [self.temporal_binding.output_length(f) for f in frames]
 
+    def _local_global(self, x: torch.Tensor, lengths):
+        """(local features, fused features): the local stack then the global context, with the
+        stack's final LayerNorm and the context's query LayerNorm in one launch
+        (VASR_LN_PAIR=0: two)."""
+        gc = self.global_context
+        if os.environ.get("VASR_LN_PAIR", "1") != "0" and type(gc.norm2) is nn.LayerNorm \
+                and type(self.local_ssm.norm) is nn.LayerNorm:
+            local, query = self.local_ssm.forward_pair(x, gc.norm2)
+            return local, gc(local, lengths=lengths, query=query)
+        local = self.local_ssm(x)
+        return local, gc(local, lengths=lengths)
+
     def forward(self, mel_spectrogram: torch.Tensor, return_features: bool = False, frames=None):
         """(B, frames, mel_bins) -> CTC logits (B, (frames + 1) // 2, vocab_size).
 
@@ -214,8 +226,7 @@ class VELOCITYASR(nn.Module):
         lengths = self._token_lengths(frames, mel.shape[1])
         with torch.no_grad():
             x = self.temporal_binding(mel)
-            local_features = self.local_ssm(x)
-            fused_features = self.global_context(local_features, lengths=lengths)
+            local_features, fused_features = self._local_global(x, lengths)
             logits = self.ctc_head(fused_features)
         if return_features:
             return logits, {"temporal_binding": x, "local_features": local_features,
@@ -232,8 +243,7 @@ class VELOCITYASR(nn.Module):
         lengths = self._token_lengths(frames, mel_spectrogram.shape[1])
         with torch.no_grad():
             x = self.temporal_binding(mel_spectrogram.to(torch.float32))
-            x = self.local_ssm(x)
-            x = self.global_context(x, lengths=lengths)
+            x = self._local_global(x, lengths)[1]
             return self.ctc_head.argmax(x)
 
     def greedy_token_ids(self, mel_spectrogram: torch.Tensor, frames=None, blank: int = 0, out=None, rows=None):
@@ -246,8 +256,7 @@ class VELOCITYASR(nn.Module):
         lengths = self._token_lengths(frames, mel_spectrogram.shape[1])
         with torch.no_grad():
             x = self.temporal_binding(mel_spectrogram.to(torch.float32))
-            x = self.local_ssm(x)
-            x = self.global_context(x, lengths=lengths)
+            x = self._local_global(x, lengths)[1]
             return self.ctc_head.greedy(x, blank, out=out, rows=rows)
 
     def get_output_length(self, input_length: int) -> int:

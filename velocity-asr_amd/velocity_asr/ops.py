@@ -402,6 +402,22 @@ def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1
     return y.view(*x.shape[:-1], C) if out is None else out
 
 
+def layer_norm_pair(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, eps1: float, w2: torch.Tensor,
+                    b2: torch.Tensor, eps2: float):
+    """(LN1(x), LN2(LN1(x))) in one launch, each bitwise layer_norm's (vasr_layer_norm_pair_f32)."""
+    _cuda_f32("layer_norm_pair.x", x)
+    w1, b1, w2, b2 = f32(w1), f32(b1), f32(w2), f32(b2)
+    C = x.shape[-1]
+    x2 = x.reshape(-1, C)
+    rows, _, ldx = _rows("layer_norm_pair.x", x2)
+    y1 = torch.empty((rows, C), device=x.device, dtype=torch.float32)
+    y2 = torch.empty((rows, C), device=x.device, dtype=torch.float32)
+    check(L.lib().vasr_layer_norm_pair_f32(x2.data_ptr(), ldx, w1.data_ptr(), b1.data_ptr(), float(eps1),
+                                           y1.data_ptr(), C, w2.data_ptr(), b2.data_ptr(), float(eps2),
+                                           y2.data_ptr(), C, rows, C, stream_of(x)), "vasr_layer_norm_pair_f32")
+    return y1.view(*x.shape[:-1], C), y2.view(*x.shape[:-1], C)
+
+
 def add_table(x: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
     """x (B, L, C) + table (L, C) broadcast over the batch."""
     _cuda_f32("add_table.x", x)

@@ -321,6 +321,14 @@ class LocalSSMProcessor(nn.Module):
             x = layer(x)
         return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
 
+    def forward_pair(self, x: torch.Tensor, norm2: nn.LayerNorm):
+        """(forward(x), norm2(forward(x))) with both LayerNorms in one launch (the global context's
+        query norm right after this stack's final one, ops.layer_norm_pair): bitwise the same."""
+        for layer in self.layers:
+            x = layer(x)
+        return ops.layer_norm_pair(x, self.norm.weight, self.norm.bias, self.norm.eps, norm2.weight, norm2.bias,
+                                   norm2.eps)
+
 
 class GlobalSSM(nn.Module):
     """SSM over pooled tokens; always the default 'parallel' scan (reference ssm.py:508-556)."""
