@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 17
+#define VASR_ABI_VERSION 18
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -167,6 +167,15 @@ int vasr_add_table_f32(const float* x, const float* table, float* out, int B, in
 int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b,
                        const float* conv_w, const float* conv_b, float* y,
                        int B, int L, int C, int Kc, float eps, void* stream);
+
+/* vasr_ln_dwconv_f32 on LN0(x) without the LN0 launch: xo = LN0(x; pre_w, pre_b, pre_eps) (the
+ * temporal binding's LayerNorm, reference model.py:200, applied to its conv + GELU + PE rows) is
+ * formed in registers, stored once (the first SSM block's residual input) and fed to norm1 + the
+ * causal conv: xo and y bitwise vasr_layer_norm_f32 followed by vasr_ln_dwconv_f32.  C = 192,
+ * Kc = 4 (the model's); x, xo, y distinct. */
+int vasr_ln_dwconv_prenorm_f32(const float* x, const float* pre_w, const float* pre_b, float pre_eps, float* xo,
+                               const float* ln_w, const float* ln_b, const float* conv_w, const float* conv_b,
+                               float* y, int B, int L, int C, int Kc, float eps, void* stream);
 
 /* ------------------------------------------------------------------ selective scan
  * SelectiveSSM scan + D skip + SiLU gate (ssm.py:119-129):

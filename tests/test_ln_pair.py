@@ -1,6 +1,10 @@
-"""The paired LayerNorm (vasr_layer_norm_pair_f32): the local stack's final norm and the global
-context's query norm in one launch.  Both outputs bitwise equal to two vasr_layer_norm_f32 calls,
-and the model's logits / tokens bitwise equal with the pair on (VASR_LN_PAIR=1, default) and off."""
+"""LayerNorms folded into neighbouring launches, each bitwise the separate launches:
+* the paired LayerNorm (vasr_layer_norm_pair_f32): the local stack's final norm and the global
+  context's query norm in one launch (VASR_LN_PAIR);
+* the temporal binding's LayerNorm inside the first SSM block's norm1 + conv launch
+  (vasr_ln_dwconv_prenorm_f32, VASR_TB_PRENORM).
+The model's logits / tokens are compared with each fold on and off, and against forward(...,
+return_features=True), which runs every LayerNorm as its own launch."""
 import pytest
 import torch
 
@@ -41,8 +45,38 @@ def test_layer_norm_pair_argument_checks():
                                         None) == -1
 
 
-@pytest.mark.parametrize("B,S", [(2, 48000), (32, 160000)])
-def test_model_ln_pair_bitwise(monkeypatch, B, S):
+@pytest.mark.parametrize("B,L", [(1, 1), (1, 5), (2, 37), (3, 129), (32, 501)])
+def test_ln_dwconv_prenorm_bitwise(B, L):
+    from velocity_asr import _lib, ops
+    g = torch.Generator(device=DEV).manual_seed(B * 1000 + L)
+    C = 192
+    x = torch.randn(B, L, C, device=DEV, generator=g) * 2 + 0.3
+    rn = lambda *s, sc=0.2: torch.randn(*s, device=DEV, generator=g) * sc  # noqa: E731
+    pw, pb, lw, lb, cw, cb = 1 + rn(C), rn(C), 1 + rn(C), rn(C), rn(C, 4, sc=0.5), rn(C)
+    ref_x = ops.layer_norm(x, pw, pb, 1e-5)
+    for rows in (0, 4, 8, 16):
+        with ops.option(_lib.OPT_DW_ROWS, rows):
+            y, xo = ops.ln_dwconv_prenorm(x, pw, pb, 1e-5, lw, lb, cw, cb, 1e-6)
+            ref_y = ops.ln_dwconv(ref_x, lw, lb, cw, cb, 1e-6)
+        assert torch.equal(xo, ref_x), rows
+        assert torch.equal(y, ref_y), rows
+
+
+def test_ln_dwconv_prenorm_argument_checks():
+    from velocity_asr import _lib
+    lib = _lib.lib()
+    x = torch.zeros(4 * 192, device=DEV)
+    p, q, r = x.data_ptr(), x[192:].data_ptr(), x[384:].data_ptr()
+    assert lib.vasr_ln_dwconv_prenorm_f32(p, p, p, 1e-5, q, p, p, p, p, None, 1, 1, 192, 4, 1e-5, None) == -1
+    assert b"null" in lib.vasr_last_error()
+    assert lib.vasr_ln_dwconv_prenorm_f32(p, p, p, 1e-5, p, p, p, p, p, r, 1, 1, 192, 4, 1e-5, None) == -1
+    assert b"distinct" in lib.vasr_last_error()
+    assert lib.vasr_ln_dwconv_prenorm_f32(p, p, p, 1e-5, q, p, p, p, p, r, 1, 1, 128, 4, 1e-5, None) == -1
+    assert lib.vasr_ln_dwconv_prenorm_f32(p, p, p, 1e-5, q, p, p, p, p, r, 1, 1, 192, 3, 1e-5, None) == -1
+
+
+@pytest.mark.parametrize("B,S", [(1, 16000), (2, 48000), (32, 160000)])
+def test_model_ln_folds_bitwise(monkeypatch, B, S):
     import velocity_asr as va
     from velocity_asr import synthetic as S_
     W = S_.make_weights(None, seed=0)
@@ -50,13 +84,14 @@ def test_model_ln_pair_bitwise(monkeypatch, B, S):
     m.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()}, strict=True)
     m = m.to(DEV).eval()
     mel = va.compute_mel_spectrogram(torch.from_numpy(S_.make_audio(B, S, seed=99)).to(DEV))
-    monkeypatch.setenv("VASR_LN_PAIR", "1")
-    a, fa = m(mel, return_features=True)
-    ta = m.greedy_token_ids(mel)
-    monkeypatch.setenv("VASR_LN_PAIR", "0")
-    b, fb = m(mel, return_features=True)
-    tb = m.greedy_token_ids(mel)
-    assert torch.equal(fa["local_features"], fb["local_features"])
-    assert torch.equal(a, b)
-    assert torch.equal(ta[1], tb[1])  # collapsed lengths; tokens past them are unwritten
-    assert all(torch.equal(ta[0][i, :n], tb[0][i, :n]) for i, n in enumerate(ta[1].tolist()))
+    ref, _ = m(mel, return_features=True)  # every LayerNorm its own launch
+    runs = []
+    for pair, pre in (("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")):
+        monkeypatch.setenv("VASR_LN_PAIR", pair)
+        monkeypatch.setenv("VASR_TB_PRENORM", pre)
+        runs.append((m(mel), m.greedy_token_ids(mel), m.token_ids(mel)))
+    for logits, (tok, n), ids in runs:
+        assert torch.equal(logits, ref)
+        assert torch.equal(ids, runs[0][2])
+        assert torch.equal(n, runs[0][1][1])  # collapsed lengths; tokens past them are unwritten
+        assert all(torch.equal(tok[i, :k], runs[0][1][0][i, :k]) for i, k in enumerate(n.tolist()))

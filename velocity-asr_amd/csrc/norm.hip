@@ -33,7 +33,11 @@ __device__ __forceinline__ void ln_vals(float (&v)[ln_per_lane<CPL>()], const fl
     for (int i = 0; i < PL; ++i) {
         const int c = i * 64 + lane;
         const float d = (CPL > 0 || c < C) ? v[i] - mean : 0.f;
-        q += d * d;
+        // explicit fma chain (q starts at 0: the first term is d * d rounded once): a bare
+        // q += d * d may be contracted in one kernel and SLP-packed into separate multiplies and
+        // adds in another, which moved some rows' variance by an ulp between the kernels that
+        // share this function
+        q = __builtin_fmaf(d, d, q);
     }
     const float var = wave_sum(q) / (float)C;
     const float rstd = 1.0f / sqrtf(var + eps);
@@ -123,13 +127,22 @@ constexpr int kMaxK = 8;
 // 0 = generic (C <= kMaxC, guarded columns).  The channel's taps and bias are loaded before
 // phase 1 (C <= kMaxC = 256 threads: one channel per thread), so their latency overlaps the
 // row loads instead of following the barrier.
-template <int KC, int CPT, int TT>
+//
+// PRE (C = 64 * CPT only): x is the row before a LayerNorm of its own (pre_w, pre_b, pre_eps: the
+// temporal binding's norm, model.py), applied to every tile row in registers before norm1 with
+// layer_norm_kernel's own arithmetic (ln_vals), and the block's own rows of it stored to xo (the
+// SSM block's residual input): bitwise the LayerNorm launch + this kernel on its output.
+template <int KC, int CPT, int TT, bool PRE = false>
 __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ ln_w,
                                                         const float* __restrict__ ln_b,
                                                         const float* __restrict__ cw,
                                                         const float* __restrict__ cb, float* __restrict__ y,
-                                                        int L, int C, int Kc_rt, float eps) {
+                                                        int L, int C, int Kc_rt, float eps,
+                                                        const float* __restrict__ pre_w = nullptr,
+                                                        const float* __restrict__ pre_b = nullptr, float pre_eps = 0.f,
+                                                        float* __restrict__ xo = nullptr) {
+    static_assert(!PRE || CPT > 0, "the pre-norm needs C = 64 * CPT");
     const int Kc = KC > 0 ? KC : Kc_rt;
     constexpr int KM = KC > 0 ? KC : kMaxK;
     __shared__ float tile[(TT + KM - 1) * kMaxC];
@@ -169,6 +182,17 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
             v[i][c] = (ok && (CPT > 0 || col < C)) ? xb[(int64_t)t * C + col] : 0.f;
         }
     }
+    if constexpr (PRE) {
+        float* xob = xo + (int64_t)b * L * C;
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int rr = wave + 4 * i;
+            if (rr >= nrows) continue;  // wave-uniform
+            ln_vals<CPT>(v[i], pre_w, pre_b, C, pre_eps, lane);
+            const int t = t0 - (Kc - 1) + rr;
+            if (rr >= Kc - 1) ln_store<CPT>(v[i], xob + (int64_t)t * C, C, lane);  // this block's own rows
+        }
+    }
     float mean[RPW], rstd[RPW];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
@@ -183,7 +207,7 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const float d = (CPT > 0 || c * 64 + lane < C) ? v[i][c] - mean[i] : 0.f;
-            q += d * d;
+            q = __builtin_fmaf(d, d, q);  // as ln_vals: the same rounding in every instantiation
         }
         rstd[i] = 1.0f / sqrtf(wave_sum(q) / (float)C + eps);
     }
@@ -300,6 +324,29 @@ VASR_API int vasr_layer_norm_pair_f32(const float* x, int64_t ldx, const float* 
     }
 #undef VASR_LN2
     return launch_status("vasr_layer_norm_pair_f32");
+}
+
+VASR_API int vasr_ln_dwconv_prenorm_f32(const float* x, const float* pre_w, const float* pre_b, float pre_eps,
+                                        float* xo, const float* ln_w, const float* ln_b, const float* conv_w,
+                                        const float* conv_b, float* y, int B, int L, int C, int Kc, float eps,
+                                        void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && pre_w && pre_b && xo && ln_w && ln_b && conv_w && conv_b && y,
+                   "vasr_ln_dwconv_prenorm_f32: null pointer");
+    VASR_CHECK_ARG(x != y && x != xo && xo != y, "vasr_ln_dwconv_prenorm_f32: x, xo and y must be distinct");
+    VASR_CHECK_ARG(C == 192 && Kc == 4 && B >= 0 && L >= 0,
+                   "vasr_ln_dwconv_prenorm_f32: C = 192 and Kc = 4 only (C=%d Kc=%d)", C, Kc);
+    if (B == 0 || L == 0) return VASR_OK;
+    const dim3 block(256);
+    hipStream_t s = as_stream(stream);
+    const int n16 = B * ((L + 15) / 16);
+    const int tt = option(VASR_OPT_DW_ROWS) ? option(VASR_OPT_DW_ROWS) : n16 < 128 ? 4 : n16 < 1024 ? 8 : 16;
+#define VASR_DWP(TT)                                                                                              \
+    hipLaunchKernelGGL((ln_dwconv_kernel<4, 3, TT, true>), dim3((L + TT - 1) / TT, B), block, 0, s, x, ln_w, ln_b, \
+                       conv_w, conv_b, y, L, C, Kc, eps, pre_w, pre_b, pre_eps, xo)
+    if (tt == 4) VASR_DWP(4); else if (tt == 8) VASR_DWP(8); else VASR_DWP(16);
+#undef VASR_DWP
+    return launch_status("vasr_ln_dwconv_prenorm_f32");
 }
 
 VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b, const float* conv_w,

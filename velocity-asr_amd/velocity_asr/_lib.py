@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -60,6 +60,8 @@ _SIGNATURES = {
     "vasr_layer_norm_pair_f32": ([c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, c_p, c_p, c_f32, c_p, c_i64, ctypes.c_int,
                                   ctypes.c_int, c_p], ctypes.c_int),
     "vasr_add_table_f32": ([c_p, c_p, c_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_p], ctypes.c_int),
+    "vasr_ln_dwconv_prenorm_f32": ([c_p, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p, c_p] + [ctypes.c_int] * 4
+                                   + [c_f32, c_p], ctypes.c_int),
     "vasr_ln_dwconv_f32": ([c_p, c_p, c_p, c_p, c_p, c_p] + [ctypes.c_int] * 4 + [c_f32, c_p], ctypes.c_int),
     "vasr_ssm_scan_f32": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64] + [ctypes.c_int] * 5 + [c_p],
                           ctypes.c_int),

@@ -103,7 +103,9 @@ class TemporalBindingLayer(nn.Module):
         k, s, p = c.kernel_size[0], c.stride[0], c.padding[0]
         return (frames + 2 * p - k) // s + 1
 
-    def forward(self, mel_spectrogram: torch.Tensor) -> torch.Tensor:
+    def forward(self, mel_spectrogram: torch.Tensor, raw: bool = False) -> torch.Tensor:
+        """raw (extension): the rows before the final LayerNorm (the first SSM block applies it
+        inside its own first launch, VELOCITYASR._local_global)."""
         D = Q.inner(self.conv).out_channels
         L = self.output_length(mel_spectrogram.shape[1])
         if Q.observing(self.conv):
@@ -111,6 +113,8 @@ class TemporalBindingLayer(nn.Module):
         # conv (+ activation fake-quant for QuantizedConv1d) -> GELU -> + PE, one GEMM
         x = Q.conv1d_rows(self.conv, mel_spectrogram, epilogue=_lib.EPI_GELU_PE, aux=self.pos_encoding.table(L),
                           ld_aux=D)
+        if raw:
+            return x
         return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
 
 
@@ -199,16 +203,22 @@ class VELOCITYASR(nn.Module):
             raise ValueError(f"frames: each utterance needs 1..{n_frames} frames, got {frames}")
         return [self.temporal_binding.output_length(f) for f in frames]
 
-    def _local_global(self, x: torch.Tensor, lengths):
-        """(local features, fused features): the local stack then the global context, with the
-        stack's final LayerNorm and the context's query LayerNorm in one launch
-        (VASR_LN_PAIR=0: two)."""
-        gc = self.global_context
+    def _local_global(self, mel: torch.Tensor, lengths):
+        """mel -> (local features, fused features): the temporal binding, the local stack, then the
+        global context.  The stack's final LayerNorm and the context's query LayerNorm run as one
+        launch (VASR_LN_PAIR=0: two), and the temporal binding's LayerNorm inside the first block's
+        norm1 + conv launch (VASR_TB_PRENORM=0: its own launch); bitwise the same either way."""
+        gc, tb = self.global_context, self.temporal_binding
+        pre = None
+        if os.environ.get("VASR_TB_PRENORM", "1") != "0" and type(tb.norm) is nn.LayerNorm:
+            x, pre = tb(mel, raw=True), tb.norm
+        else:
+            x = tb(mel)
         if os.environ.get("VASR_LN_PAIR", "1") != "0" and type(gc.norm2) is nn.LayerNorm \
                 and type(self.local_ssm.norm) is nn.LayerNorm:
-            local, query = self.local_ssm.forward_pair(x, gc.norm2)
+            local, query = self.local_ssm.forward_pair(x, gc.norm2, pre_norm=pre)
             return local, gc(local, lengths=lengths, query=query)
-        local = self.local_ssm(x)
+        local = self.local_ssm(x, pre_norm=pre)
         return local, gc(local, lengths=lengths)
 
     def forward(self, mel_spectrogram: torch.Tensor, return_features: bool = False, frames=None):
@@ -225,8 +235,12 @@ class VELOCITYASR(nn.Module):
         mel = mel_spectrogram.to(torch.float32)
         lengths = self._token_lengths(frames, mel.shape[1])
         with torch.no_grad():
-            x = self.temporal_binding(mel)
-            local_features, fused_features = self._local_global(x, lengths)
+            if return_features:  # the temporal binding's rows are returned, so they are formed on their own
+                x = self.temporal_binding(mel)
+                local_features = self.local_ssm(x)
+                fused_features = self.global_context(local_features, lengths=lengths)
+            else:
+                local_features, fused_features = self._local_global(mel, lengths)
             logits = self.ctc_head(fused_features)
         if return_features:
             return logits, {"temporal_binding": x, "local_features": local_features,
@@ -242,8 +256,7 @@ class VELOCITYASR(nn.Module):
             raise RuntimeError("velocity_asr (MI355X build): token_ids needs HIP tensors")
         lengths = self._token_lengths(frames, mel_spectrogram.shape[1])
         with torch.no_grad():
-            x = self.temporal_binding(mel_spectrogram.to(torch.float32))
-            x = self._local_global(x, lengths)[1]
+            x = self._local_global(mel_spectrogram.to(torch.float32), lengths)[1]
             return self.ctc_head.argmax(x)
 
     def greedy_token_ids(self, mel_spectrogram: torch.Tensor, frames=None, blank: int = 0, out=None, rows=None):
@@ -255,8 +268,7 @@ class VELOCITYASR(nn.Module):
             raise RuntimeError("velocity_asr (MI355X build): greedy_token_ids needs HIP tensors")
         lengths = self._token_lengths(frames, mel_spectrogram.shape[1])
         with torch.no_grad():
-            x = self.temporal_binding(mel_spectrogram.to(torch.float32))
-            x = self._local_global(x, lengths)[1]
+            x = self._local_global(mel_spectrogram.to(torch.float32), lengths)[1]
             return self.ctc_head.greedy(x, blank, out=out, rows=rows)
 
     def get_output_length(self, input_length: int) -> int:

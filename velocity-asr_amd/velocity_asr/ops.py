@@ -447,6 +447,24 @@ def ln_dwconv(x: torch.Tensor, ln_w, ln_b, conv_w, conv_b, eps: float = 1e-5) ->
     return y
 
 
+def ln_dwconv_prenorm(x: torch.Tensor, pre_w, pre_b, pre_eps: float, ln_w, ln_b, conv_w, conv_b,
+                      eps: float = 1e-5):
+    """(B, L, 192) -> (ln_dwconv(LN0(x)), LN0(x)) without LN0's own launch (vasr_ln_dwconv_prenorm_f32):
+    both bitwise layer_norm + ln_dwconv.  Kc = 4 only."""
+    _cuda_f32("ln_dwconv_prenorm.x", x)
+    pre_w, pre_b = f32(pre_w), f32(pre_b)
+    ln_w, ln_b, conv_w, conv_b = f32(ln_w), f32(ln_b), f32(conv_w), f32(conv_b)
+    x = x.contiguous()
+    B, Lq, C = x.shape
+    Kc = conv_w.shape[-1]
+    y, xo = torch.empty_like(x), torch.empty_like(x)
+    check(L.lib().vasr_ln_dwconv_prenorm_f32(x.data_ptr(), pre_w.data_ptr(), pre_b.data_ptr(), float(pre_eps),
+                                             xo.data_ptr(), ln_w.data_ptr(), ln_b.data_ptr(),
+                                             conv_w.contiguous().data_ptr(), conv_b.data_ptr(), y.data_ptr(), B, Lq, C,
+                                             Kc, float(eps), stream_of(x)), "vasr_ln_dwconv_prenorm_f32")
+    return y, xo
+
+
 # Chunk-parallel tree scan (vasr_ssm_scan_chunked_f32, bitwise equal to the streaming kernel)
 # for launches under CHUNKED_MAX_WAVES waves of the streaming kernel (B * Di * N / 256 at 4 states
 # per lane) over more than CHUNKED_MIN_L steps: one utterance at a time, as the reference's

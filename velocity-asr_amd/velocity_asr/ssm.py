@@ -17,7 +17,7 @@ from __future__ import annotations
 import math
 import os
 import warnings
-from typing import Literal
+from typing import Literal, Optional
 
 import torch
 import torch.nn as nn
@@ -205,12 +205,15 @@ class SSMBlock(nn.Module):
                 and tuple(w.shape) == (384, 192) and self.ssm.d_inner == 384
                 and self.ssm.out_proj.weight.dtype == w.dtype == self.ffn[3].weight.dtype)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, pre_norm: Optional[nn.LayerNorm] = None) -> torch.Tensor:
+        """pre_norm (extension): x is the temporal binding's row before its final LayerNorm, which
+        this block applies inside its norm1 + conv launch (_norm_conv); the result is bitwise the
+        same as for pre_norm(x)."""
         _check_eval(self)
         B, L, D = x.shape
         if self._z_in_tail(B, L, D):
-            return self._forward_z_in_tail(x)
-        x2, xz, xdt = self.head(x)
+            return self._forward_z_in_tail(x, pre_norm)
+        x2, xz, xdt = self.head(x, pre_norm)
         g = self.ssm.scan(xz, xdt, B, L)
         return self.tail(g, x2, B, L)
 
@@ -245,15 +248,28 @@ class SSMBlock(nn.Module):
             return False
         return ("w_noz" if dtype == torch.float32 else "w_x") in ssm._prepared()
 
-    def _forward_z_in_tail(self, x: torch.Tensor) -> torch.Tensor:
+    def _norm_conv(self, x: torch.Tensor, pre_norm: Optional[nn.LayerNorm]):
+        """(conv(norm1(x)), x) as (B, L, D) tensors; with pre_norm, x is first pre_norm(x), formed
+        inside the same launch when the shape allows it (vasr_ln_dwconv_prenorm_f32: D = 192, 4
+        taps), else by its own LayerNorm launch."""
+        B, L, D = x.shape
+        x = x.contiguous()
+        cw = ops.f32(self.conv.weight).view(D, -1)
+        if pre_norm is not None:
+            if D == 192 and cw.shape[1] == 4:
+                return ops.ln_dwconv_prenorm(x, pre_norm.weight, pre_norm.bias, pre_norm.eps, self.norm1.weight,
+                                             self.norm1.bias, cw, self.conv.bias, self.norm1.eps)
+            x = ops.layer_norm(x, pre_norm.weight, pre_norm.bias, pre_norm.eps)
+        return ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, cw, self.conv.bias, self.norm1.eps), x
+
+    def _forward_z_in_tail(self, x: torch.Tensor, pre_norm: Optional[nn.LayerNorm] = None) -> torch.Tensor:
         B, L, D = x.shape
         ssm = self.ssm
         Di, N = ssm.d_inner, ssm.state_dim
         p = ssm._prepared()
-        x = x.contiguous()
+        u, x = self._norm_conv(x, pre_norm)
         x2 = x.view(B * L, D)
-        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
-                          self.conv.bias, self.norm1.eps).view(B * L, D)
+        u = u.view(B * L, D)
         if "w_noz" in p or ("w_noz16" in p and _bf16_compose()):
             w, b = (p["w_noz"], p["b_noz"]) if "w_noz" in p else (p["w_noz16"], p["b_noz16"])
             xbd = ops.gemm(u, w, b, epilogue=_lib.EPI_SOFTPLUS_FROM, n_out=Di + 2 * N)  # [x|B|C|dt]
@@ -273,14 +289,12 @@ class SSMBlock(nn.Module):
     # + residual, LN2, FFN + residual).  (Issuing one utterance group's scans on a stream of their
     # own beside the other group's heads and tails measured slower than independent group
     # streams: profiles/r02_paired/.)
-    def head(self, x: torch.Tensor):
-        """x (B, L, D) -> (x2 = x as (B*L, D) rows, xz, xdt): the scan's operands."""
+    def head(self, x: torch.Tensor, pre_norm: Optional[nn.LayerNorm] = None):
+        """x (B, L, D) -> (x2 = x as (B*L, D) rows, xz, xdt): the scan's operands (pre_norm: forward's)."""
         _check_eval(self)
         B, L, D = x.shape
-        x = x.contiguous()
+        u, x = self._norm_conv(x, pre_norm)
         x2 = x.view(B * L, D)
-        u = ops.ln_dwconv(x, self.norm1.weight, self.norm1.bias, ops.f32(self.conv.weight).view(D, -1),
-                          self.conv.bias, self.norm1.eps)
         xz, xdt = self.ssm.project(u.view(B * L, D))
         return x2, xz, xdt
 
@@ -316,16 +330,18 @@ class LocalSSMProcessor(nn.Module):
         ])
         self.norm = nn.LayerNorm(d_model)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        for layer in self.layers:
-            x = layer(x)
+    def forward(self, x: torch.Tensor, pre_norm: Optional[nn.LayerNorm] = None) -> torch.Tensor:
+        """pre_norm (extension): the LayerNorm still to be applied to x, folded into the first
+        block's norm1 + conv launch (SSMBlock.forward)."""
+        for i, layer in enumerate(self.layers):
+            x = layer(x, pre_norm) if i == 0 else layer(x)
         return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
 
-    def forward_pair(self, x: torch.Tensor, norm2: nn.LayerNorm):
+    def forward_pair(self, x: torch.Tensor, norm2: nn.LayerNorm, pre_norm: Optional[nn.LayerNorm] = None):
         """(forward(x), norm2(forward(x))) with both LayerNorms in one launch (the global context's
         query norm right after this stack's final one, ops.layer_norm_pair): bitwise the same."""
-        for layer in self.layers:
-            x = layer(x)
+        for i, layer in enumerate(self.layers):
+            x = layer(x, pre_norm) if i == 0 else layer(x)
         return ops.layer_norm_pair(x, self.norm.weight, self.norm.bias, self.norm.eps, norm2.weight, norm2.bias,
                                    norm2.eps)
 
