@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VASR_ABI_VERSION 18
+#define VASR_ABI_VERSION 19
 
 #define VASR_OK 0
 #define VASR_EINVAL (-1)
@@ -358,6 +358,14 @@ int vasr_adaptive_pool_f32(const float* x, float* out, int B, int L, int C, int 
  * <= L, ks[b] <= K), bins past ks[b] written as 0; x and out keep the strides L and K. */
 int vasr_adaptive_pool_var_f32(const float* x, float* out, int B, int L, int C, int K, const int32_t* lens,
                                const int32_t* ks, void* stream);
+
+/* LayerNorm(x; w, b, eps) of every row, then vasr_adaptive_pool_f32 (lens / ks null) or
+ * vasr_adaptive_pool_var_f32 (both given) of the normalised rows, in one launch without the
+ * normalised rows in memory: bitwise vasr_layer_norm_f32 followed by the pooling.  Replaces the
+ * global SSM stack's final norm (reference ssm.py:555) followed by the second pooling level's
+ * average pool (attention.py:303, AdaptivePool.forward :69-73).  C <= 1024. */
+int vasr_ln_adaptive_pool_f32(const float* x, const float* w, const float* b, float eps, float* out, int B, int L,
+                              int C, int K, const int32_t* lens, const int32_t* ks, void* stream);
 
 /* Pooled multi-head cross attention core (attention.py:143-160), no mask:
  * out[b,t,h*hd:(h+1)*hd] = softmax(q_bth . k_bh^T / sqrt(hd)) v_bh over the Kp pooled keys.

@@ -107,6 +107,54 @@ __global__ __launch_bounds__(256) void layer_norm_pair_kernel(const float* __res
     ln_store<CPL>(v, y2 + (int64_t)row * ldy2, C, lane);
 }
 
+// LayerNorm of every row, then F.adaptive_avg_pool1d over time (vasr_adaptive_pool_f32's windows and
+// in-order sums): the global SSM stack's final norm followed by the second pooling level
+// (attention.py).  One wave per (utterance, bin); the window's rows are loaded G at a time before
+// they are normalised (ln_vals, layer_norm_kernel's own arithmetic) and added in row order, so the
+// result is bitwise the LayerNorm launch + the pooling launch.  lens / ks as adaptive_pool_kernel.
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_adaptive_pool_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ bias, float eps,
+                                                               float* __restrict__ out, int B, int L, int C, int K,
+                                                               const int32_t* __restrict__ lens,
+                                                               const int32_t* __restrict__ ks) {
+    constexpr int PL = ln_per_lane<CPL>();
+    constexpr int G = CPL > 0 ? 8 : 1;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= B * K) return;
+    const int lane = threadIdx.x & 63;
+    const int b = row / K, i = row - b * K;
+    const int Lb = lens ? lens[b] : L, Kb = ks ? ks[b] : K;
+    float acc[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) acc[k] = 0.f;
+    float* o = out + (int64_t)row * C;
+    if (i >= Kb) {
+        ln_store<CPL>(acc, o, C, lane);
+        return;
+    }
+    const int s = (int)(((int64_t)i * Lb) / Kb);
+    const int e = (int)(((int64_t)(i + 1) * Lb + Kb - 1) / Kb);
+    const float* xb = x + (int64_t)b * L * C;
+    for (int t0 = s; t0 < e; t0 += G) {
+        float v[G][PL];
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            if (t0 + j < e) ln_load<CPL>(v[j], xb + (int64_t)(t0 + j) * C, C, lane);
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            if (t0 + j < e) {  // wave-uniform
+                ln_vals<CPL>(v[j], w, bias, C, eps, lane);
+#pragma unroll
+                for (int k = 0; k < PL; ++k) acc[k] += v[j][k];
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) acc[k] = acc[k] / (float)(e - s);
+    ln_store<CPL>(acc, o, C, lane);
+}
+
 // TT: output rows per block -- 16 for full-chip launches (1024 blocks at B = 32, L = 501: 4 per
 // CU), 8 below 1024 blocks of 16, 4 below 128 (graph-timed at L = 501, bitwise the same outputs:
 // B = 1 2.74 / 3.18 / 4.09 us at 4 / 8 / 16 rows, B = 16 5.69 / 5.28 / 5.65, B = 32 9.11 / 8.39 /
@@ -347,6 +395,28 @@ VASR_API int vasr_ln_dwconv_prenorm_f32(const float* x, const float* pre_w, cons
     if (tt == 4) VASR_DWP(4); else if (tt == 8) VASR_DWP(8); else VASR_DWP(16);
 #undef VASR_DWP
     return launch_status("vasr_ln_dwconv_prenorm_f32");
+}
+
+VASR_API int vasr_ln_adaptive_pool_f32(const float* x, const float* w, const float* b, float eps, float* out, int B,
+                                       int L, int C, int K, const int32_t* lens, const int32_t* ks, void* stream) {
+    using namespace vasr;
+    VASR_CHECK_ARG(x && w && b && out, "vasr_ln_adaptive_pool_f32: null pointer");
+    VASR_CHECK_ARG((lens == nullptr) == (ks == nullptr), "vasr_ln_adaptive_pool_f32: lens and ks go together");
+    VASR_CHECK_ARG(B >= 0 && L >= 1 && C >= 1 && C <= 64 * kMaxPerLane && K >= 1 && K <= L,
+                   "vasr_ln_adaptive_pool_f32: need 1 <= K <= L and C <= %d (K=%d L=%d C=%d)", 64 * kMaxPerLane, K, L,
+                   C);
+    if (B == 0) return VASR_OK;
+    const dim3 grid((unsigned)(((int64_t)B * K + 3) / 4)), block(256);
+    hipStream_t s = as_stream(stream);
+    switch (C) {
+        case 192:
+            hipLaunchKernelGGL(ln_adaptive_pool_kernel<3>, grid, block, 0, s, x, w, b, eps, out, B, L, C, K, lens, ks);
+            break;
+        default:
+            hipLaunchKernelGGL(ln_adaptive_pool_kernel<0>, grid, block, 0, s, x, w, b, eps, out, B, L, C, K, lens, ks);
+            break;
+    }
+    return launch_status("vasr_ln_adaptive_pool_f32");
 }
 
 VASR_API int vasr_ln_dwconv_f32(const float* x, const float* ln_w, const float* ln_b, const float* conv_w,

@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # VASR_LIB overrides the library path (diagnostic builds of the same sources, tools/).
 LIB_PATH = os.environ.get("VASR_LIB") or os.path.join(_HERE, "lib", "libvasr_hip.so")
@@ -100,6 +100,7 @@ _SIGNATURES = {
     "vasr_ctc_collapse_var": ([c_p, ctypes.c_int, ctypes.c_int, c_p, ctypes.c_int, ctypes.c_int, c_p, c_p, c_p, c_p,
                                c_p], ctypes.c_int),
     "vasr_pad_frames_f32": ([c_p, c_p] + [ctypes.c_int] * 5 + [c_p], ctypes.c_int),
+    "vasr_ln_adaptive_pool_f32": ([c_p, c_p, c_p, c_f32, c_p] + [ctypes.c_int] * 4 + [c_p, c_p, c_p], ctypes.c_int),
     "vasr_adaptive_pool_f32": ([c_p, c_p] + [ctypes.c_int] * 4 + [c_p], ctypes.c_int),
     "vasr_pooled_attention_f32": ([c_p, c_i64, c_p, c_p] + [ctypes.c_int] * 5 + [c_p], ctypes.c_int),
     "vasr_argmax_f32": ([c_p, c_i64, ctypes.c_int, ctypes.c_int, c_p, c_p], ctypes.c_int),

@@ -9,6 +9,7 @@ gate, local and global branches in registers (no (B, L, 2D) concat, no gate tens
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -40,20 +41,27 @@ class AdaptivePool(nn.Module):
         k1 = prev_pool_size if prev_pool_size else max(64, seq_len // 8)
         return min(64, max(16, k1 // 4))
 
-    def forward(self, x: torch.Tensor, prev_pool_size=None, lengths: Optional[Sequence[int]] = None):
+    def forward(self, x: torch.Tensor, prev_pool_size=None, lengths: Optional[Sequence[int]] = None,
+                pre_norm: Optional[nn.LayerNorm] = None):
         """(B, L, D) -> ((B, K, D), K).  lengths: per-utterance valid rows of a zero-padded batch
         (prev_pool_size then per utterance too): each utterance is pooled to the size it gets
-        alone, rows past it are junk nobody reads, and the sizes are returned as a list."""
+        alone, rows past it are junk nobody reads, and the sizes are returned as a list.
+        pre_norm (extension): x is the row before that LayerNorm, applied inside the pooling launch
+        (ops.ln_adaptive_pool), bitwise the same as pooling pre_norm(x)."""
         B, L, D = x.shape
+
+        def pool(K, lens=None, ks=None):
+            if pre_norm is None:
+                return ops.adaptive_pool(x, K, lens=lens, ks=ks)
+            return ops.ln_adaptive_pool(x, pre_norm.weight, pre_norm.bias, pre_norm.eps, K, lens=lens, ks=ks)
         if lengths is None:
             pool_size = min(self._compute_pool_size(L, prev_pool_size), L)
-            pooled = ops.adaptive_pool(x, pool_size)
+            pooled = pool(pool_size)
         else:
             prev = prev_pool_size if prev_pool_size is not None else [None] * B
             sizes = [min(self._compute_pool_size(n, p), n) for n, p in zip(lengths, prev)]
             pool_size = max(sizes)
-            pooled = ops.adaptive_pool(x, pool_size, lens=_device_ints(lengths, x.device),
-                                       ks=_device_ints(sizes, x.device))
+            pooled = pool(pool_size, lens=_device_ints(lengths, x.device), ks=_device_ints(sizes, x.device))
         w, b, qp = Q.linear_parts(self.pool_proj)
         out = ops.gemm(pooled.view(B * pool_size, D), w, b, qparams=qp)
         Q.record(self.pool_proj, out)
@@ -184,7 +192,6 @@ class GatedFusion(nn.Module):
     def composable(self, mha: "MultiHeadAttention") -> bool:
         """forward_attention applies: plain Linears (no QAT fake-quant on global_context or the
         fusion's inputs), one weight dtype; VASR_ATTN_COMPOSE=0 keeps the separate out_proj."""
-        import os
         mods = (mha.out_proj, self.gate_proj[0], self.local_proj, self.global_proj, self.out_proj)
         return (os.environ.get("VASR_ATTN_COMPOSE", "1") != "0" and all(type(m) is nn.Linear for m in mods)
                 and len({m.weight.dtype for m in mods}) == 1 and mha.out_proj.bias is not None)
@@ -254,9 +261,15 @@ class HierarchicalGlobalContext(nn.Module):
         query (extension): norm2(local_features) when the caller already has it
         (LocalSSMProcessor.forward_pair)."""
         x_pool1, pool_size1 = self.pool1(local_features, lengths=lengths)
-        x_ssm = self.global_ssm(x_pool1)
+        # VASR_POOL_PRENORM=1: the global stack's final LayerNorm inside the second pooling launch
+        # (bitwise the same; off by default: C2 -0.2 %, C3 -0.5 % interleaved, profiles/r06bd/ --
+        # 512 waves each normalising its window's rows serially lose to two wide launches)
+        gnorm = self.global_ssm.norm
+        fold = os.environ.get("VASR_POOL_PRENORM", "0") == "1" and type(gnorm) is nn.LayerNorm
+        x_ssm = self.global_ssm(x_pool1, raw=fold)
         x_pool2, pool_size2 = self.pool2(x_ssm, prev_pool_size=pool_size1,
-                                         lengths=None if lengths is None else pool_size1)
+                                         lengths=None if lengths is None else pool_size1,
+                                         pre_norm=gnorm if fold else None)
         x_pool2 = ops.layer_norm(x_pool2, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         if query is None:
             query = ops.layer_norm(local_features, self.norm2.weight, self.norm2.bias, self.norm2.eps)

@@ -742,6 +742,27 @@ def adaptive_pool(x: torch.Tensor, K: int, lens: Optional[torch.Tensor] = None,
     return out
 
 
+def ln_adaptive_pool(x: torch.Tensor, w, b, eps: float, K: int, lens: Optional[torch.Tensor] = None,
+                     ks: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """adaptive_pool(layer_norm(x, w, b, eps), K, lens, ks) in one launch, bitwise the two
+    (vasr_ln_adaptive_pool_f32)."""
+    _cuda_f32("ln_adaptive_pool.x", x)
+    w, b = f32(w), f32(b)
+    x = x.contiguous()
+    B, Lq, C = x.shape
+    out = torch.empty((B, K, C), device=x.device, dtype=torch.float32)
+    if (lens is None) != (ks is None):
+        raise ValueError("ln_adaptive_pool: lens and ks go together")
+    if lens is not None:
+        lens = _lens("ln_adaptive_pool.lens", lens, B, x.device)
+        ks = _lens("ln_adaptive_pool.ks", ks, B, x.device)
+    check(L.lib().vasr_ln_adaptive_pool_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), float(eps), out.data_ptr(), B,
+                                            Lq, C, K, None if lens is None else lens.data_ptr(),
+                                            None if ks is None else ks.data_ptr(), stream_of(x)),
+          "vasr_ln_adaptive_pool_f32")
+    return out
+
+
 def pooled_attention(q: torch.Tensor, kv: torch.Tensor, B: int, Lq: int, Kp: int, heads: int,
                      kps: Optional[torch.Tensor] = None) -> torch.Tensor:
     """kps: per-utterance key counts (int32 (B,), each in [1, Kp])."""

@@ -357,7 +357,11 @@ class GlobalSSM(nn.Module):
         ])
         self.norm = nn.LayerNorm(d_model)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, raw: bool = False) -> torch.Tensor:
+        """raw (extension): the rows before the final LayerNorm (the global context applies it
+        inside its second pooling launch)."""
         for layer in self.layers:
             x = layer(x)
+        if raw:
+            return x
         return ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
