@@ -232,13 +232,15 @@ __global__ __launch_bounds__(256) void ln_dwconv_kernel(const float* __restrict_
     }
     if constexpr (PRE) {
         float* xob = xo + (int64_t)b * L * C;
+        // every row slot normalised (rows past the tile hold zeros: finite, never stored or used),
+        // so the slots' reduction chains carry no branches between them and interleave
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) ln_vals<CPT>(v[i], pre_w, pre_b, C, pre_eps, lane);
 #pragma unroll
         for (int i = 0; i < RPW; ++i) {
             const int rr = wave + 4 * i;
-            if (rr >= nrows) continue;  // wave-uniform
-            ln_vals<CPT>(v[i], pre_w, pre_b, C, pre_eps, lane);
             const int t = t0 - (Kc - 1) + rr;
-            if (rr >= Kc - 1) ln_store<CPT>(v[i], xob + (int64_t)t * C, C, lane);  // this block's own rows
+            if (rr >= Kc - 1 && rr < nrows) ln_store<CPT>(v[i], xob + (int64_t)t * C, C, lane);  // own rows
         }
     }
     float mean[RPW], rstd[RPW];
