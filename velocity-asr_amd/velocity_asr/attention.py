@@ -261,9 +261,10 @@ class HierarchicalGlobalContext(nn.Module):
         query (extension): norm2(local_features) when the caller already has it
         (LocalSSMProcessor.forward_pair)."""
         x_pool1, pool_size1 = self.pool1(local_features, lengths=lengths)
-        # VASR_POOL_PRENORM=1: the global stack's final LayerNorm inside the second pooling launch
-        # (bitwise the same; off by default: C2 -0.2 %, C3 -0.5 % interleaved, profiles/r06bd/ --
-        # 512 waves each normalising its window's rows serially lose to two wide launches)
+        # VASR_POOL_PRENORM=1: the global stack's final LayerNorm inside the second pooling launch.
+        # Bitwise the same, and 3.5 vs 5.3 us graph-timed alone at C2's 32 x 64 -> 16 rows, but C2
+        # 0.3 % slower in the model's graph over three interleaved rounds (profiles/r06bh/, r06bi/):
+        # off by default
         gnorm = self.global_ssm.norm
         fold = os.environ.get("VASR_POOL_PRENORM", "0") == "1" and type(gnorm) is nn.LayerNorm
         x_ssm = self.global_ssm(x_pool1, raw=fold)
